@@ -1,0 +1,161 @@
+/*
+ * pfscdc.h — C ABI of the MI355X PFS chunk-ingest path (libpfscdc.so).
+ *
+ * Drop-in boundary for the reference's chunk layer.  The reference has no FFI on this path
+ * (pure Go, no cgo); its seam is the Go type chunk.Writer.  Each entry point below names
+ * the reference interface it replaces (paths under /root/reference).  Plain pointers and
+ * sizes only; no torch or HIP types cross this boundary except the opaque stream handle.
+ *
+ * Status codes: 0 = ok, negative = error (PFSCDC_E*).  Errors are sticky on a writer, like
+ * chunk.Writer.err (src/internal/storage/chunk/writer.go:145-161).
+ * Threading: a ctx (and its writers) is owned by one thread at a time; one ctx per GPU;
+ * distinct ctxs may run concurrently (independent chunk.Writers, chunk/storage.go:60-66).
+ */
+#ifndef PFSCDC_H
+#define PFSCDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFSCDC_OK 0
+#define PFSCDC_EINVAL -1      /* bad argument */
+#define PFSCDC_EHIP -2        /* HIP runtime error (see pfscdc_last_error) */
+#define PFSCDC_ENOMEM -3      /* device or host allocation failed */
+#define PFSCDC_EUNSUPPORTED -4 /* configuration the GPU path does not implement */
+#define PFSCDC_ESTATE -5      /* call order violated (e.g. Write before Annotate) */
+#define PFSCDC_ECALLBACK -6   /* the writer callback returned non-zero */
+
+/* chunk.WithRollingHashConfig(averageBits, seed) + chunk.WithMinMax(min, max)
+ * (chunk/option.go:50-64); defaults writer.go:39-44: 23, 1, 1 MB, 20 MB (decimal). */
+typedef struct pfscdc_params {
+  uint32_t average_bits; /* split mask = 2^bits - 1, avg = 2^bits (1..32) */
+  uint32_t reserved;
+  int64_t seed;          /* buzhash64.GenerateHashes seed */
+  int64_t min_chunk;     /* must be >= 64 (the window) on the GPU path */
+  int64_t max_chunk;
+} pfscdc_params;
+
+/* One segment = the bytes of one file (annotation) inside one chunk = one DataRef
+ * (writer.go:288-312: DataRef.Hash = BLAKE2b-256 of exactly these bytes). */
+typedef struct pfscdc_segment {
+  uint64_t offset;  /* offset of the segment inside its file */
+  uint64_t size;    /* bytes */
+  uint32_t file;    /* index of the file in the batch */
+  uint32_t flags;   /* PFSCDC_SEG_* */
+  uint8_t hash[32]; /* BLAKE2b-256 (pachhash.Sum, pachhash/hash.go:27-30) */
+} pfscdc_segment;   /* 56 bytes */
+
+#define PFSCDC_SEG_VALID 1u
+#define PFSCDC_SEG_CUT 2u /* the segment ends on a CDC cut (else: at end of file) */
+
+typedef struct pfscdc_ctx pfscdc_ctx;
+
+/* Fills params with the reference defaults (writer.go:39-44). */
+void pfscdc_default_params(pfscdc_params* p);
+
+/* buzhash64.GenerateHashes(seed) (called at chunk/option.go:54). */
+int pfscdc_table(int64_t seed, uint64_t out[256]);
+
+/* First n values of Go's rand.NewSource(seed).Int63() (known-answer hook for tests). */
+int pfscdc_go_int63(int64_t seed, int64_t* out, int n);
+
+/* Replaces chunk.Storage.NewWriter's per-writer config (chunk/storage.go:60-66,
+ * writer.go:74-98): binds params and a GPU.  device = HIP ordinal. */
+int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out);
+int pfscdc_ctx_destroy(pfscdc_ctx* ctx);
+const char* pfscdc_last_error(const pfscdc_ctx* ctx);
+
+/* Run every following GPU call of ctx on this hipStream_t (NULL = the ctx's own stream). */
+int pfscdc_set_stream(pfscdc_ctx* ctx, void* hip_stream);
+
+/* CDC + content hash of a batch of files (one annotation each, concatenated).
+ * Replaces, for every file of the batch, Writer.Annotate + Writer.Write + the hash part of
+ * processChunk (writer.go:118-143,163-196,233-253,288-312): per-file cut positions and
+ * per-segment BLAKE2b-256.  bytes: nbytes bytes, device pointer (16-B aligned) if
+ * bytes_on_device else host memory (copied with hipMemcpyAsync).  file_offsets: host array
+ * of nfiles+1 nondecreasing offsets, file_offsets[0] == 0, file_offsets[nfiles] == nbytes.
+ * Blocks until the segment records are on the host; read them with pfscdc_segments. */
+int pfscdc_scan(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                const uint64_t* file_offsets, uint32_t nfiles);
+
+/* Asynchronous form: enqueue on the ctx stream; pfscdc_wait() completes it. */
+int pfscdc_scan_async(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes,
+                      int bytes_on_device, const uint64_t* file_offsets, uint32_t nfiles);
+int pfscdc_wait(pfscdc_ctx* ctx);
+
+/* Results of the last completed scan, ordered by (file, offset).  Valid until the next
+ * scan on ctx.  seg_begin[f]..seg_begin[f+1] index file f's segments (nfiles+1 entries). */
+uint64_t pfscdc_num_segments(const pfscdc_ctx* ctx);
+const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* ctx);
+const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* ctx);
+
+/* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
+ * positions inside dense tiles are reported through the tile marker instead.  Debug/test
+ * hook for the candidate-scan kernel. */
+uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
+
+/* Device timing of the last scan's kernels (ms, HIP events on the ctx stream):
+ * out[0] candidate scan, out[1] compaction, out[2] selection, out[3] BLAKE2b, out[4] total. */
+int pfscdc_last_timings(pfscdc_ctx* ctx, float out[5]);
+
+/* Pinned host memory for staging (PCIe-inclusive end-to-end path). */
+void* pfscdc_host_alloc(uint64_t nbytes);
+void pfscdc_host_free(void* p);
+
+/* Synthetic data generator used by bench/tests (device-side): word k of file f is
+ * splitmix64-finalize((f << 40 | k) + (seed + 1) * 0x9E3779B97F4A7C15), little endian.
+ * Writes every file of file_offsets into dev_bytes on the ctx stream. */
+int pfscdc_fill_synthetic(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* file_offsets,
+                          uint32_t nfiles, uint64_t seed);
+
+/* ---- chunk.Writer mirror (writer.go:52-438) ------------------------------------------
+ * A writer buffers annotated bytes in host memory, runs them through pfscdc_scan in
+ * batches of whole files, assembles chunks exactly as createChunk/Annotate do (including
+ * multi-file chunks, the buf.Len() >= avg cut before a file, edge flags and the empty last
+ * chunk of Close) and invokes the callback serially in chunk order, like TaskChain
+ * (chunk/chain.go:55-68). */
+
+typedef struct pfscdc_dataref {
+  uint8_t hash[32];      /* DataRef.Hash */
+  int64_t offset_bytes;  /* DataRef.OffsetBytes (offset inside the chunk) */
+  int64_t size_bytes;    /* DataRef.SizeBytes */
+} pfscdc_dataref;
+
+typedef struct pfscdc_chunk_ref {
+  uint64_t chunk_index;  /* 0-based order of createChunk calls */
+  int64_t size_bytes;    /* Ref.SizeBytes (== plaintext size: CreateOptions{} => no gzip) */
+  int32_t edge;          /* Ref.Edge = first || last (writer.go:200) */
+  int32_t reserved;
+} pfscdc_chunk_ref;
+
+typedef struct pfscdc_annotation_out {
+  uint64_t user;         /* Annotation.Data: the id passed to pfscdc_writer_annotate */
+  int32_t has_data_ref;  /* 0 => NextDataRef == nil (size-0 piece) */
+  int32_t reserved;
+  pfscdc_dataref data_ref;
+} pfscdc_annotation_out;
+
+/* WriterCallback (writer.go:31): annotations of one chunk, in order.  Non-zero aborts. */
+typedef int (*pfscdc_writer_cb)(void* user, const pfscdc_chunk_ref* chunk,
+                                const pfscdc_annotation_out* annotations, uint32_t n);
+
+typedef struct pfscdc_writer pfscdc_writer;
+
+/* batch_bytes: flush threshold for buffered file bytes (0 = 1 GiB). */
+int pfscdc_writer_create(pfscdc_ctx* ctx, pfscdc_writer_cb cb, void* user,
+                         uint64_t batch_bytes, pfscdc_writer** out);
+int pfscdc_writer_annotate(pfscdc_writer* w, uint64_t user);            /* writer.go:118 */
+int pfscdc_writer_write(pfscdc_writer* w, const void* data, uint64_t n); /* writer.go:132 */
+int pfscdc_writer_close(pfscdc_writer* w);                               /* writer.go:423 */
+int64_t pfscdc_writer_chunk_count(const pfscdc_writer* w);               /* writer.go:113 */
+int64_t pfscdc_writer_annotation_count(const pfscdc_writer* w);          /* writer.go:107 */
+int pfscdc_writer_destroy(pfscdc_writer* w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFSCDC_H */

@@ -1,0 +1,158 @@
+"""ctypes binding of libpfscdc.so (the C ABI declared in include/pfscdc.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) and loaded from this
+package directory.  There is no fallback: if the library is missing or a call fails, the
+caller gets an exception.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpfscdc.so")
+
+PFSCDC_OK = 0
+PFSCDC_EINVAL = -1
+PFSCDC_EHIP = -2
+PFSCDC_ENOMEM = -3
+PFSCDC_EUNSUPPORTED = -4
+PFSCDC_ESTATE = -5
+PFSCDC_ECALLBACK = -6
+
+SEG_VALID = 1
+SEG_CUT = 2
+
+# Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
+EXPORTED = [
+    "pfscdc_default_params", "pfscdc_table", "pfscdc_go_int63", "pfscdc_ctx_create",
+    "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_scan",
+    "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
+    "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
+    "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_writer_create",
+    "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
+    "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
+]
+
+
+class Params(C.Structure):
+    _fields_ = [("average_bits", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_int64),
+                ("min_chunk", C.c_int64), ("max_chunk", C.c_int64)]
+
+
+class Segment(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("size", C.c_uint64), ("file", C.c_uint32),
+                ("flags", C.c_uint32), ("hash", C.c_uint8 * 32)]
+
+
+class DataRef(C.Structure):
+    _fields_ = [("hash", C.c_uint8 * 32), ("offset_bytes", C.c_int64), ("size_bytes", C.c_int64)]
+
+
+class ChunkRef(C.Structure):
+    _fields_ = [("chunk_index", C.c_uint64), ("size_bytes", C.c_int64), ("edge", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class AnnotationOut(C.Structure):
+    _fields_ = [("user", C.c_uint64), ("has_data_ref", C.c_int32), ("reserved", C.c_int32),
+                ("data_ref", DataRef)]
+
+
+assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32
+
+WRITER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(ChunkRef), C.POINTER(AnnotationOut),
+                        C.c_uint32)
+
+# numpy view of pfscdc_segment
+SEGMENT_DTYPE = None
+
+
+def segment_dtype():
+    global SEGMENT_DTYPE
+    if SEGMENT_DTYPE is None:
+        import numpy as np
+        SEGMENT_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8"), ("file", "<u4"),
+                                  ("flags", "<u4"), ("hash", "u1", (32,))])
+        assert SEGMENT_DTYPE.itemsize == 56
+    return SEGMENT_DTYPE
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+class PfsCdcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pfscdc error {code}: {msg}")
+        self.code = code
+
+
+def load() -> C.CDLL:
+    """Load libpfscdc.so (raises if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make` or "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = C.CDLL(LIB_PATH)
+        u64, i64, u32, i32, vp = C.c_uint64, C.c_int64, C.c_uint32, C.c_int, C.c_void_p
+        P = C.POINTER
+        sig = {
+            "pfscdc_default_params": (None, [P(Params)]),
+            "pfscdc_table": (i32, [i64, P(u64)]),
+            "pfscdc_go_int63": (i32, [i64, P(i64), i32]),
+            "pfscdc_ctx_create": (i32, [P(Params), i32, P(vp)]),
+            "pfscdc_ctx_destroy": (i32, [vp]),
+            "pfscdc_last_error": (C.c_char_p, [vp]),
+            "pfscdc_set_stream": (i32, [vp, vp]),
+            "pfscdc_scan": (i32, [vp, vp, u64, i32, P(u64), u32]),
+            "pfscdc_scan_async": (i32, [vp, vp, u64, i32, P(u64), u32]),
+            "pfscdc_wait": (i32, [vp]),
+            "pfscdc_num_segments": (u64, [vp]),
+            "pfscdc_segments": (P(Segment), [vp]),
+            "pfscdc_file_segment_begin": (P(u64), [vp]),
+            "pfscdc_debug_candidates": (u64, [vp, P(u64), u64]),
+            "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
+            "pfscdc_host_alloc": (vp, [u64]),
+            "pfscdc_host_free": (None, [vp]),
+            "pfscdc_fill_synthetic": (i32, [vp, vp, P(u64), u32, u64]),
+            "pfscdc_writer_create": (i32, [vp, WRITER_CB, vp, u64, P(vp)]),
+            "pfscdc_writer_annotate": (i32, [vp, u64]),
+            "pfscdc_writer_write": (i32, [vp, vp, u64]),
+            "pfscdc_writer_close": (i32, [vp]),
+            "pfscdc_writer_chunk_count": (i64, [vp]),
+            "pfscdc_writer_annotation_count": (i64, [vp]),
+            "pfscdc_writer_destroy": (i32, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def default_params() -> Params:
+    p = Params()
+    load().pfscdc_default_params(C.byref(p))
+    return p
+
+
+def table(seed: int) -> list[int]:
+    out = (C.c_uint64 * 256)()
+    rc = load().pfscdc_table(seed, out)
+    if rc:
+        raise PfsCdcError(rc, "pfscdc_table")
+    return list(out)
+
+
+def go_int63(seed: int, n: int) -> list[int]:
+    out = (C.c_int64 * n)()
+    rc = load().pfscdc_go_int63(seed, out, n)
+    if rc:
+        raise PfsCdcError(rc, "pfscdc_go_int63")
+    return list(out)

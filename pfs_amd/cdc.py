@@ -1,0 +1,159 @@
+"""Batch CDC + content-hash API over libpfscdc (one GPU per ``Chunker``).
+
+``Chunker.scan`` is the batch form of the reference's per-file ``Writer.Annotate`` +
+``Writer.Write`` + ``processChunk`` hashing (/root/reference/src/internal/storage/chunk/
+writer.go:118-196,233-312): it returns, for every file of the batch, its segments (the
+bytes of that file inside one chunk, i.e. one DataRef) with their BLAKE2b-256 digests.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class ChunkParams:
+    """chunk.WithRollingHashConfig + WithMinMax (chunk/option.go:50-64); defaults writer.go:39-44."""
+    average_bits: int = 23
+    seed: int = 1
+    min_chunk: int = 1_000_000
+    max_chunk: int = 20_000_000
+
+    def to_c(self) -> _lib.Params:
+        return _lib.Params(self.average_bits, 0, self.seed, self.min_chunk, self.max_chunk)
+
+
+@dataclass
+class ScanResult:
+    segments: np.ndarray        # structured SEGMENT_DTYPE, ordered by (file, offset)
+    file_begin: np.ndarray      # uint64[nfiles+1]: file f owns segments[file_begin[f]:file_begin[f+1]]
+    timings_ms: Optional[dict] = None
+
+    def file_segments(self, f: int) -> np.ndarray:
+        return self.segments[int(self.file_begin[f]):int(self.file_begin[f + 1])]
+
+
+def _offsets_array(file_offsets: Sequence[int]) -> np.ndarray:
+    offs = np.ascontiguousarray(np.asarray(file_offsets, dtype=np.uint64))
+    if offs.ndim != 1 or len(offs) < 1:
+        raise ValueError("file_offsets must be a 1-D sequence of nfiles+1 offsets")
+    return offs
+
+
+class Chunker:
+    """A GPU context bound to one device and one parameter set."""
+
+    def __init__(self, params: ChunkParams = ChunkParams(), device: int = 0):
+        self.lib = _lib.load()
+        self.params = params
+        self.device = device
+        ctx = C.c_void_p()
+        p = params.to_c()
+        rc = self.lib.pfscdc_ctx_create(C.byref(p), device, C.byref(ctx))
+        if rc:
+            raise _lib.PfsCdcError(rc, "pfscdc_ctx_create failed (no GPU or bad params)")
+        self.ctx = ctx
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.pfscdc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc:
+            msg = self.lib.pfscdc_last_error(self.ctx)
+            raise _lib.PfsCdcError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def set_stream(self, stream_handle: Optional[int]) -> None:
+        self._check(self.lib.pfscdc_set_stream(self.ctx, stream_handle or None), "set_stream")
+
+    def scan_async(self, data, file_offsets: Sequence[int]) -> None:
+        """Enqueue a batch.  ``data``: bytes/bytearray/np.uint8 array (host) or a torch uint8
+        CUDA tensor (device-resident, 16-byte aligned)."""
+        offs = _offsets_array(file_offsets)
+        self._offs_keep = offs
+        nfiles = len(offs) - 1
+        on_dev = 0
+        if hasattr(data, "is_cuda") and data.is_cuda:
+            if data.dtype.itemsize != 1 or not data.is_contiguous():
+                raise ValueError("device data must be a contiguous uint8 tensor")
+            ptr, nbytes, on_dev = data.data_ptr(), data.numel(), 1
+            self._data_keep = data
+        else:
+            arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+                else np.ascontiguousarray(data, dtype=np.uint8)
+            self._data_keep = arr
+            ptr, nbytes = (arr.ctypes.data if arr.size else None), arr.size
+        rc = self.lib.pfscdc_scan_async(self.ctx, ptr, nbytes, on_dev,
+                                        offs.ctypes.data_as(C.POINTER(C.c_uint64)), nfiles)
+        self._check(rc, "scan_async")
+        self._nfiles = nfiles
+
+    def wait(self) -> ScanResult:
+        self._check(self.lib.pfscdc_wait(self.ctx), "wait")
+        n = self.lib.pfscdc_num_segments(self.ctx)
+        dt = _lib.segment_dtype()
+        if n:
+            ptr = self.lib.pfscdc_segments(self.ctx)
+            buf = C.string_at(ptr, n * dt.itemsize)
+            segs = np.frombuffer(buf, dtype=dt).copy()
+        else:
+            segs = np.zeros(0, dtype=dt)
+        bp = self.lib.pfscdc_file_segment_begin(self.ctx)
+        begin = np.ctypeslib.as_array(bp, shape=(self._nfiles + 1,)).copy() if bp else \
+            np.zeros(self._nfiles + 1, dtype=np.uint64)
+        return ScanResult(segs, begin)
+
+    def scan(self, data, file_offsets: Sequence[int]) -> ScanResult:
+        self.scan_async(data, file_offsets)
+        return self.wait()
+
+    def timings(self) -> dict:
+        out = (C.c_float * 5)()
+        self._check(self.lib.pfscdc_last_timings(self.ctx, out), "timings")
+        return dict(zip(["scan", "compact", "select", "hash", "total"], list(out)))
+
+    def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
+        out = (C.c_uint64 * cap)()
+        n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)
+        return np.array(out[:min(n, cap)], dtype=np.uint64)
+
+    def fill_synthetic(self, tensor, file_offsets: Sequence[int], seed: int) -> None:
+        """Fill a torch uint8 CUDA tensor with the synthetic byte stream (see pfscdc.h)."""
+        offs = _offsets_array(file_offsets)
+        rc = self.lib.pfscdc_fill_synthetic(self.ctx, tensor.data_ptr(),
+                                            offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            len(offs) - 1, seed)
+        self._check(rc, "fill_synthetic")
+
+
+def synthetic_bytes(file_offsets: Sequence[int], seed: int) -> np.ndarray:
+    """Host copy of the synthetic stream (same definition as the device generator)."""
+    offs = np.asarray(file_offsets, dtype=np.uint64)
+    out = np.empty(int(offs[-1]), dtype=np.uint8)
+    gamma = np.uint64((seed + 1) * 0x9E3779B97F4A7C15 % (1 << 64))
+    for f in range(len(offs) - 1):
+        a, b = int(offs[f]), int(offs[f + 1])
+        n = b - a
+        if n == 0:
+            continue
+        nw = (n + 7) // 8
+        with np.errstate(over="ignore"):
+            z = (np.uint64(f) << np.uint64(40)) | np.arange(nw, dtype=np.uint64)
+            z = z + gamma
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+        out[a:b] = z.astype("<u8").view(np.uint8)[:n]
+    return out

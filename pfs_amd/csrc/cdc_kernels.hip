@@ -1,0 +1,659 @@
+// cdc_kernels.hip — gfx950 kernels of the PFS chunk-ingest path.
+//
+// Reference path replaced (paths under /root/reference):
+//   chunk.Writer.roll            src/internal/storage/chunk/writer.go:163-189  (CDC)
+//   buzhash64 Roll/Sum64         third-party rollinghash v4.0.0, writer.go:166-167
+//   chunk.Hash / pachhash.Sum    chunk/metadata.go:16-20, pachhash/hash.go:27-30 (BLAKE2b-256)
+//   newDataRef hashing           writer.go:240,301-312
+//
+// Pipeline for one batch (files concatenated in HBM):
+//   1. cdc_scan_kernel     every byte: h_i = XOR_{k<64} rotl64(T[x_{i-k}], k), candidate iff
+//                          h_i & mask == 0.  Lane = 4 KiB strip, 64-byte halo re-read;
+//                          rolling recurrence; T replicated 32x in LDS so ds_read_b64 is
+//                          bank-conflict free; per 2 MiB tile <= 15 sorted candidates or a
+//                          DENSE flag.  HBM-bound by design (1 byte read per file byte).
+//   2. compact_kernel      one workgroup: prefix sum over tiles -> sorted candidate list.
+//   3. select_kernel       one wave per file: serial cut selection over the sparse list
+//                          (writer.go:168,179 min/max rule), dense tiles re-rolled in-wave.
+//   4. segcompact_kernel   one workgroup: per-file segment counts -> dense segment list.
+//   5. blake2b_kernel      4 lanes per segment (one BLAKE2b column each, DPP quad
+//                          rotations for the diagonal step), message via LDS.
+// Why the hash of a cut only needs the last 64 bytes: min >= 64 and hash+seglen reset at
+// every Annotate/cut (writer.go:125-128,211), so no eligible position sees the reset window.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pfscdc_internal.h"
+
+#define PFS_DEV __device__ __forceinline__
+
+namespace pfscdc {
+
+// ------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------
+
+PFS_DEV uint64_t rotl1_64(uint64_t x) { return (x << 1) | (x >> 63); }
+
+// LDS byte address of T[byte j of w] in this lane's copy: (idx << 8) | (lane & 31) * 8.
+PFS_DEV uint32_t tab_addr(uint32_t w, uint32_t lane_off, int j) {
+  return __builtin_amdgcn_perm(w, lane_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
+}
+
+template <typename T>
+PFS_DEV T lds_load(const uint8_t* lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const T*>(lds + byte_addr);
+}
+
+// LDS read at an absolute LDS byte address (the scan kernel's dynamic LDS starts at 0: it
+// declares no static __shared__), so no base add is emitted.
+typedef __attribute__((address_space(3))) const uint64_t lds_u64_t;
+PFS_DEV uint64_t lds_abs_u64(uint32_t a) { return *(lds_u64_t*)(uintptr_t)a; }
+
+// gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is a 3-input XOR.
+PFS_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+PFS_DEV void load64(uint32_t (&w)[16], const uint8_t* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const u32x4 v = __builtin_nontemporal_load(q + i);  // file bytes are read exactly once
+    w[4 * i + 0] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+PFS_DEV uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t lo = __shfl_xor((uint32_t)v, o, 64);
+    uint32_t hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+    uint64_t u = ((uint64_t)hi << 32) | lo;
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. candidate scan
+// ------------------------------------------------------------------------------------------
+
+// One rolling step: h = rotl(h,1) ^ T[in] ^ T[out]   (buzhash64 Roll with window 64)
+#define PFS_ROLL(WIN, WOUT, J)                                                   \
+  do {                                                                           \
+    const uint64_t ti_ = lds_abs_u64(tab_addr((WIN), lane_off, (J)));            \
+    const uint64_t to_ = lds_abs_u64(tab_addr((WOUT), lane_off, (J)));           \
+    const uint32_t nl_ = __builtin_amdgcn_alignbit(hl, hh, 31);                  \
+    const uint32_t nh_ = __builtin_amdgcn_alignbit(hh, hl, 31);                  \
+    hl = xor3(nl_, (uint32_t)ti_, (uint32_t)to_);                                \
+    hh = xor3(nh_, (uint32_t)(ti_ >> 32), (uint32_t)(to_ >> 32));                \
+  } while (0)
+
+template <bool WIDE>
+PFS_DEV uint32_t cand_key(uint32_t hl, uint32_t hh, uint32_t kshift) {
+  // zero iff (h & mask) == 0; narrow: bits <= 32, key = hl << (32 - bits)
+  if (WIDE) return hl | (hh << kshift);
+  return hl << kshift;
+}
+
+// Source of the 64-byte block at absolute offset p: the file bytes below n_main (n rounded
+// down to 64), else the zero-padded tail copy (so the loop never needs guarded loads).
+PFS_DEV const uint8_t* block_src(const uint8_t* data, const uint8_t* tail, uint64_t n_main,
+                                 uint64_t p) {
+  return p < n_main ? data + p : tail + (p - n_main);
+}
+
+// Rare path: a block had a candidate; re-roll it byte by byte from its entry state and
+// record exact in-tile offsets (writer.go:167 test, positions >= 63 and < n only).  Bytes
+// are re-read from memory so the hot loop's register blocks are never indexed dynamically.
+PFS_DEV void record_block(const uint8_t* __restrict__ data,
+                                          const uint8_t* __restrict__ tail, uint64_t n_main,
+                                          uint64_t h, uint64_t pos, uint64_t n,
+                                          uint64_t tile_base, uint64_t mask64,
+                                          const uint64_t* __restrict__ table,
+                                          uint32_t* s_count, uint32_t* s_cand) {
+  const uint8_t* in = block_src(data, tail, n_main, pos);
+  const uint8_t* out = pos >= 64 ? block_src(data, tail, n_main, pos - 64) : nullptr;
+  for (int t = 0; t < 64; t++) {
+    const uint64_t i = pos + t;
+    const uint32_t bi = in[t];
+    const uint32_t bo = out ? out[t] : 0u;
+    h = rotl1_64(h) ^ table[bi] ^ table[bo];
+    if ((h & mask64) == 0 && i >= 63 && i < n) {
+      const uint32_t k = atomicAdd(s_count, 1u);
+      if (k < kTileCandCap) s_cand[k] = (uint32_t)(i - tile_base);
+    }
+  }
+}
+
+// One 64-byte block: prefetch the block after it into NXT, roll IN against OUT (the block
+// 64 bytes earlier supplies the outgoing bytes), test all 64 positions with one min-reduce.
+#define PFS_SCAN_BLOCK(IN, OUT, NXT)                                                     \
+  {                                                                                      \
+    if (pos >= s1) break;                                                                \
+    load64(NXT, block_src(data, tail, n_main, pos + 64));                                \
+    const uint32_t hl0 = hl, hh0 = hh;                                                   \
+    uint32_t acc = 0xffffffffu;                                                          \
+    _Pragma("unroll") for (int t = 0; t < 64; t++) {                                     \
+      PFS_ROLL(IN[t >> 2], OUT[t >> 2], t & 3);                                          \
+      const uint32_t key = cand_key<WIDE>(hl, hh, kshift);                               \
+      acc = acc < key ? acc : key;                                                       \
+    }                                                                                    \
+    if (__builtin_expect(acc == 0, 0))                                                   \
+      record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, pos, n, tile_base,  \
+                   mask64, table, s_count, s_cand);                                      \
+    pos += 64;                                                                           \
+  }
+
+template <bool WIDE>
+__global__ __launch_bounds__(kScanBlock, 4) void cdc_scan_kernel(
+    const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
+    const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
+    TileRec* __restrict__ recs) {
+  // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then count + candidates.
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* s_count = reinterpret_cast<uint32_t*>(smem + kTableLdsBytes);
+  uint32_t* s_cand = reinterpret_cast<uint32_t*>(smem + kTableLdsBytes + 16);
+  const uint64_t n_main = n & ~63ULL;
+
+  // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
+  for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
+    const int idx = i >> 5, c = i & 31;
+    reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] = table[idx];
+  }
+  const uint32_t lane_off = (threadIdx.x & 31u) * 8u;
+
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if (threadIdx.x == 0) *s_count = 0;
+    __syncthreads();
+    const uint64_t tile_base = tile * kTile;
+    const uint64_t s0 = tile_base + (uint64_t)threadIdx.x * kStrip;
+    if (s0 < n) {
+      const uint64_t s1 = (s0 + kStrip < n) ? s0 + kStrip : n;
+      uint32_t b0[16], b1[16], b2[16];
+      if (s0 >= 64) {
+        load64(b2, block_src(data, tail, n_main, s0 - 64));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) b2[i] = 0;  // reset window (writer.go:17-19)
+      }
+      load64(b0, block_src(data, tail, n_main, s0));
+      // Write(window): h = XOR rotl(T[b_j], 63 - j) == h_{s0-1}
+      uint32_t hl = 0, hh = 0;
+#pragma unroll
+      for (int t = 0; t < 64; t++) {
+        const uint64_t ti = lds_abs_u64(tab_addr(b2[t >> 2], lane_off, t & 3));
+        const uint32_t nl = __builtin_amdgcn_alignbit(hl, hh, 31);
+        const uint32_t nh = __builtin_amdgcn_alignbit(hh, hl, 31);
+        hl = nl ^ (uint32_t)ti;
+        hh = nh ^ (uint32_t)(ti >> 32);
+      }
+      uint64_t pos = s0;
+      while (true) {
+        PFS_SCAN_BLOCK(b0, b2, b1)
+        PFS_SCAN_BLOCK(b1, b0, b2)
+        PFS_SCAN_BLOCK(b2, b1, b0)
+      }
+    }
+    __syncthreads();
+    const uint32_t cnt = *s_count;
+    TileRec* rec = recs + tile;
+    if (threadIdx.x == 0) rec->count = cnt;
+    if (cnt <= (uint32_t)kTileK && threadIdx.x < cnt) {
+      const uint32_t v = s_cand[threadIdx.x];
+      uint32_t rank = 0;
+      for (uint32_t u = 0; u < cnt; u++) rank += s_cand[u] < v;
+      rec->off[rank] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. compaction: tile records -> sorted entry list
+// ------------------------------------------------------------------------------------------
+
+// Block-wide exclusive scan (1024 threads = 16 waves); returns exclusive prefix, *total set.
+PFS_DEV uint64_t block_exclusive_scan(uint64_t v, uint64_t* s_wave, uint64_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t lo = __shfl_up((uint32_t)x, o, 64);
+    const uint32_t hi = __shfl_up((uint32_t)(x >> 32), o, 64);
+    if (lane >= o) x += ((uint64_t)hi << 32) | lo;
+  }
+  if (lane == 63) s_wave[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (int w = 0; w < kCompactBlock / 64; w++) {
+      const uint64_t t = s_wave[w];
+      s_wave[w] = run;
+      run += t;
+    }
+    s_wave[kCompactBlock / 64] = run;
+  }
+  __syncthreads();
+  const uint64_t r = s_wave[wave] + x - v;
+  *total = s_wave[kCompactBlock / 64];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kCompactBlock) void compact_kernel(
+    const TileRec* __restrict__ recs, uint64_t ntiles, uint64_t n,
+    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries) {
+  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < ntiles; base += kCompactBlock) {
+    const uint64_t t = base + threadIdx.x;
+    uint32_t c = 0;
+    uint64_t e = 0;
+    if (t < ntiles) {
+      c = recs[t].count;
+      e = c <= (uint32_t)kTileK ? c : 1;
+    }
+    uint64_t total;
+    const uint64_t ex = block_exclusive_scan(e, s_wave, &total) + carry;
+    if (t < ntiles) {
+      const uint64_t ts = t * kTile;
+      if (c <= (uint32_t)kTileK) {
+        for (uint32_t i = 0; i < c; i++) entries[ex + i] = ts + recs[t].off[i];
+      } else {
+        const uint64_t te = (ts + kTile < n) ? ts + kTile : n;
+        entries[ex] = kDenseBit | (te - 1);  // sorts as the tile's last byte
+      }
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) *n_entries = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. selection: one wave per file
+// ------------------------------------------------------------------------------------------
+
+// First candidate in [a, b] (absolute offsets, a >= 63), by re-rolling in 64 lanes.
+PFS_DEV uint64_t rescan_first(const uint8_t* __restrict__ data, const uint64_t* __restrict__ T,
+                              uint64_t a, uint64_t b, uint64_t mask) {
+  const uint32_t lane = threadIdx.x & 63u;
+  constexpr uint64_t W = 256;
+  for (uint64_t base = a; base <= b; base += 64 * W) {
+    const uint64_t st = base + lane * W;
+    const uint64_t en = (st + W - 1 < b) ? st + W - 1 : b;
+    uint64_t found = kNone;
+    if (st <= en) {
+      uint64_t h = 0;
+      for (int k = 0; k < 64; k++) h = rotl1_64(h) ^ T[data[st - 63 + k]];  // h_st
+      if ((h & mask) == 0) found = st;
+      for (uint64_t i = st + 1; found == kNone && i <= en; i++) {
+        h = rotl1_64(h) ^ T[data[i - 64]] ^ T[data[i]];
+        if ((h & mask) == 0) found = i;
+      }
+    }
+    found = wave_min_u64(found);
+    if (found != kNone) return found;
+  }
+  return kNone;
+}
+
+__global__ __launch_bounds__(kSelectBlock) void select_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ T,
+    const uint64_t* __restrict__ entries, const uint64_t* __restrict__ n_entries,
+    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ seg_base, uint32_t nfiles,
+    uint64_t mask, uint64_t min_chunk, uint64_t max_chunk,
+    pfscdc_segment* __restrict__ slots, uint64_t* __restrict__ nseg) {
+  const uint64_t f = ((uint64_t)blockIdx.x * kSelectBlock + threadIdx.x) >> 6;
+  if (f >= nfiles) return;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t fs = offs[f], fe = offs[f + 1];
+  const uint64_t sb = seg_base[f], cap = seg_base[f + 1] - sb;
+  const uint64_t ne = *n_entries;
+  pfscdc_segment* out = slots + sb;
+  uint64_t count = 0;
+  auto emit = [&](uint64_t s, uint64_t size, uint32_t flags) {
+    if (lane == 0 && count < cap) {
+      out[count].offset = s - fs;
+      out[count].size = size;
+      out[count].file = (uint32_t)f;
+      out[count].flags = flags;
+    }
+    count++;
+  };
+  // lower_bound(entries, fs + min - 1) on the entry value (dense markers = tile end)
+  uint64_t k = 0;
+  {
+    uint64_t lo = 0, hi = ne;
+    const uint64_t key = fs + min_chunk - 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((entries[mid] & ~kDenseBit) < key) lo = mid + 1;
+      else hi = mid;
+    }
+    k = lo;
+  }
+  uint64_t s = fs;
+  while (true) {
+    const uint64_t lo = s + min_chunk - 1;
+    if (lo >= fe) break;
+    const uint64_t hi = s + max_chunk - 1;
+    const uint64_t limit = hi < fe - 1 ? hi : fe - 1;
+    while (k < ne && (entries[k] & ~kDenseBit) < lo) k++;
+    uint64_t c = kNone;
+    for (uint64_t kk = k; kk < ne; kk++) {
+      const uint64_t e = entries[kk];
+      const uint64_t v = e & ~kDenseBit;
+      if (!(e & kDenseBit)) {
+        if (v <= limit) c = v;
+        break;
+      }
+      const uint64_t ts = (v / kTile) * kTile;
+      const uint64_t a = lo > ts ? lo : ts;
+      const uint64_t bnd = v < limit ? v : limit;
+      if (a <= bnd) {
+        c = rescan_first(data, T, a, bnd, mask);
+        if (c != kNone) break;
+      }
+      if (v >= limit) break;
+    }
+    uint64_t cut;
+    if (c != kNone) cut = c;
+    else if (hi <= fe - 1) cut = hi;  // forced at max (writer.go:179)
+    else break;
+    emit(s, cut + 1 - s, PFSCDC_SEG_VALID | PFSCDC_SEG_CUT);
+    s = cut + 1;
+  }
+  if (s < fe) emit(s, fe - s, PFSCDC_SEG_VALID);
+  if (lane == 0) {
+    for (uint64_t i = count; i < cap; i++) out[i].flags = 0;
+    nseg[f] = count;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. segment compaction (per-file counts -> dense list in (file, offset) order)
+// ------------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kCompactBlock) void segcompact_kernel(
+    const pfscdc_segment* __restrict__ slots, const uint64_t* __restrict__ seg_base,
+    const uint64_t* __restrict__ nseg, uint32_t nfiles, pfscdc_segment* __restrict__ segs,
+    uint64_t* __restrict__ seg_begin) {
+  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < nfiles; base += kCompactBlock) {
+    const uint64_t f = base + threadIdx.x;
+    const uint64_t c = f < nfiles ? nseg[f] : 0;
+    uint64_t total;
+    const uint64_t ex = block_exclusive_scan(c, s_wave, &total) + carry;
+    if (f < nfiles) {
+      seg_begin[f] = ex;
+      const pfscdc_segment* src = slots + seg_base[f];
+      for (uint64_t i = 0; i < c; i++) segs[ex + i] = src[i];
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) seg_begin[nfiles] = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// 5. BLAKE2b-256 per segment, 4 lanes per segment
+// ------------------------------------------------------------------------------------------
+
+__constant__ uint64_t kB2IV[8] = {
+    0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+// Per (round, lane): byte offsets (word*8) of the 4 message words the lane consumes:
+// column G_j uses sigma[r][2j], sigma[r][2j+1]; diagonal G_{4+j} uses sigma[r][8+2j], [9+2j].
+__constant__ uint32_t kSigmaPack[12][4] = {
+#define PK(a, b, c, d) ((uint32_t)(a) * 8u | (uint32_t)(b) * 8u << 8 | (uint32_t)(c) * 8u << 16 | (uint32_t)(d) * 8u << 24)
+#define ROW(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  {PK(s0, s1, s8, s9), PK(s2, s3, s10, s11), PK(s4, s5, s12, s13), PK(s6, s7, s14, s15)}
+    ROW(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15),
+    ROW(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3),
+    ROW(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4),
+    ROW(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8),
+    ROW(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13),
+    ROW(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9),
+    ROW(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11),
+    ROW(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10),
+    ROW(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5),
+    ROW(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0),
+    ROW(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15),
+    ROW(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3),
+#undef ROW
+#undef PK
+};
+
+PFS_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+template <int CTRL>
+PFS_DEV uint64_t quad_perm64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+#define PFS_G(a, b, c, d, x, y)  \
+  do {                           \
+    a = a + b + (x);             \
+    d = rotr64(d ^ a, 32);       \
+    c = c + d;                   \
+    b = rotr64(b ^ c, 24);       \
+    a = a + b + (y);             \
+    d = rotr64(d ^ a, 16);       \
+    c = c + d;                   \
+    b = rotr64(b ^ c, 63);       \
+  } while (0)
+
+// Lane q of the quad loads bytes [32q, 32q+32) of a 128-byte message block.
+PFS_DEV void msg_load_full(uint4& m0, uint4& m1, const uint8_t* p) {
+  __builtin_memcpy(&m0, p, 16);
+  __builtin_memcpy(&m1, p + 16, 16);
+}
+
+PFS_DEV void msg_load_tail(uint4& m0, uint4& m1, const uint8_t* p, int64_t avail) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t v = 0;
+    for (int b = 0; b < 4; b++)
+      if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
+    w[i] = v;
+  }
+  m0 = make_uint4(w[0], w[1], w[2], w[3]);
+  m1 = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+__global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_msg[kHashBlock / 4 * 256];
+  const uint64_t quad = ((uint64_t)blockIdx.x * kHashBlock + threadIdx.x) >> 2;
+  const uint32_t j = threadIdx.x & 3u;
+  if (quad >= *seg_count) return;  // whole quads exit together
+  pfscdc_segment* seg = segs + quad;
+  const uint64_t L = seg->size;
+  const uint8_t* src = data + offs[seg->file] + seg->offset;
+  const uint32_t slot = (threadIdx.x >> 2) * 256u;  // low byte 0: perm builds the address
+  uint8_t* my = s_msg + slot + 32u * j;
+
+  uint32_t pk[12];
+#pragma unroll
+  for (int r = 0; r < 12; r++) pk[r] = kSigmaPack[r][j];
+
+  const uint64_t iv_c = kB2IV[j];
+  const uint64_t iv_d = kB2IV[4 + j];
+  uint64_t ha = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : kB2IV[j];  // digest 32, fanout/depth 1
+  uint64_t hb = kB2IV[4 + j];
+
+  const uint64_t nblk = L == 0 ? 1 : (L + 127) / 128;
+  uint4 m0, m1;
+  if (nblk == 1) msg_load_tail(m0, m1, src + 32 * j, (int64_t)L - 32 * (int64_t)j);
+  else msg_load_full(m0, m1, src + 32 * j);
+
+  for (uint64_t blk = 0; blk < nblk; blk++) {
+    const bool last = blk + 1 == nblk;
+    reinterpret_cast<uint4*>(my)[0] = m0;
+    reinterpret_cast<uint4*>(my)[1] = m1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!last) {  // prefetch the next block into registers while this one compresses
+      const uint64_t nb = blk + 1;
+      const uint8_t* p = src + nb * 128 + 32 * j;
+      if (nb + 1 == nblk) msg_load_tail(m0, m1, p, (int64_t)(L - nb * 128) - 32 * (int64_t)j);
+      else msg_load_full(m0, m1, p);
+    }
+    const uint64_t t = last ? L : (blk + 1) * 128;
+    uint64_t a = ha, b = hb, c = iv_c;
+    uint64_t d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+      const uint32_t base = slot;
+      const uint64_t x0 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0104u));
+      const uint64_t x1 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0105u));
+      const uint64_t x2 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0106u));
+      const uint64_t x3 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0107u));
+      PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
+      b = quad_perm64<0x39>(b);            // b <- v[4+(j+1)%4]
+      c = quad_perm64<0x4E>(c);            // c <- v[8+(j+2)%4]
+      d = quad_perm64<0x93>(d);            // d <- v[12+(j+3)%4]
+      PFS_G(a, b, c, d, x2, x3);           // diagonal step: G_{4+j}
+      b = quad_perm64<0x93>(b);
+      c = quad_perm64<0x4E>(c);
+      d = quad_perm64<0x39>(d);
+    }
+    ha ^= a ^ c;
+    hb ^= b ^ d;
+  }
+  // digest = h[0..3] little endian; lane j owns h[j]
+  reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic data (bench/tests): splitmix64 finalizer of (file << 40 | word) + gamma*(seed+1)
+// ------------------------------------------------------------------------------------------
+
+PFS_DEV uint64_t synth_word(uint64_t f, uint64_t k, uint64_t seed) {
+  uint64_t z = ((f << 40) | k) + (seed + 1) * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ offs,
+                             uint32_t nfiles, uint64_t seed) {
+  const uint64_t n = offs[nfiles];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 8;
+  for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; g < n; g += stride) {
+    // file of byte g (upper_bound - 1)
+    uint32_t lo = 0, hi = nfiles;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (offs[mid] <= g) lo = mid;
+      else hi = mid;
+    }
+    uint32_t f = lo;
+    uint8_t bytes[8];
+    for (int b = 0; b < 8; b++) {
+      const uint64_t p = g + b;
+      if (p >= n) break;
+      while (f + 1 < nfiles && offs[f + 1] <= p) f++;
+      const uint64_t o = p - offs[f];
+      bytes[b] = (uint8_t)(synth_word(f, o >> 3, seed) >> (8 * (o & 7)));
+    }
+    if (g + 8 <= n) {
+      uint64_t w;
+      __builtin_memcpy(&w, bytes, 8);
+      *reinterpret_cast<uint64_t*>(out + g) = w;
+    } else {
+      for (uint64_t p = g; p < n; p++) out[p] = bytes[p - g];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers (host)
+// ------------------------------------------------------------------------------------------
+
+hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
+                       uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
+                       hipStream_t st) {
+  const size_t lds = kTableLdsBytes + 16 + 4 * kTileCandCap;
+  const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
+  if (average_bits <= 32) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)cdc_scan_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
+                                                          mask64, ntiles, recs);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)cdc_scan_kernel<true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
+                                                         mask64, ntiles, recs);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
+                          uint64_t* n_entries, hipStream_t st) {
+  compact_kernel<<<1, kCompactBlock, 0, st>>>(recs, ntiles, n, entries, n_entries);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,
+                         const uint64_t* n_entries, const uint64_t* offs,
+                         const uint64_t* seg_base, uint32_t nfiles, uint32_t average_bits,
+                         uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
+                         uint64_t* nseg, hipStream_t st) {
+  const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
+  const uint64_t waves_per_block = kSelectBlock / 64;
+  const uint64_t grid = (nfiles + waves_per_block - 1) / waves_per_block;
+  select_kernel<<<(unsigned)grid, kSelectBlock, 0, st>>>(data, d_table, entries, n_entries,
+                                                         offs, seg_base, nfiles, mask64,
+                                                         min_chunk, max_chunk, slots, nseg);
+  return hipGetLastError();
+}
+
+hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_base,
+                             const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
+                             uint64_t* seg_begin, hipStream_t st) {
+  segcompact_kernel<<<1, kCompactBlock, 0, st>>>(slots, seg_base, nseg, nfiles, segs, seg_begin);
+  return hipGetLastError();
+}
+
+hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
+                          const uint64_t* seg_count, uint64_t max_segments, hipStream_t st) {
+  if (max_segments == 0) return hipSuccess;
+  const uint64_t quads_per_block = kHashBlock / 4;
+  const uint64_t grid = (max_segments + quads_per_block - 1) / quads_per_block;
+  blake2b_kernel<<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
+                        hipStream_t st) {
+  synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, seed);
+  return hipGetLastError();
+}
+
+}  // namespace pfscdc

@@ -1,0 +1,407 @@
+// pfscdc.cpp — host side of libpfscdc.so: context, batch pipeline, C ABI.
+//
+// Replaces, per batch of files, the byte loop of chunk.Writer (reference
+// src/internal/storage/chunk/writer.go:118-196) and the hashing half of processChunk
+// (writer.go:233-253,288-312).  Chunk assembly and callbacks live in writer.cpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pfscdc_internal.h"
+
+using namespace pfscdc;
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t ensure(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1);
+    want = want + want / 4;  // amortize growth
+    hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+struct PinnedBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1);
+    want = want + want / 4;
+    hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct pfscdc_ctx {
+  pfscdc_params params{};
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  uint64_t table[256];
+  uint64_t* d_table = nullptr;
+  DevBuf<uint8_t> d_data, d_tail;
+  DevBuf<TileRec> d_recs;
+  DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
+  DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
+  DevBuf<pfscdc_segment> d_slots, d_segs;
+  PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
+  PinnedBuf<pfscdc_segment> h_segs;
+  hipEvent_t ev[6] = {};
+  bool pending = false;
+  uint32_t nfiles = 0;
+  uint64_t nbytes = 0;
+  uint64_t ntiles = 0;
+  uint64_t slot_cap = 0;
+  uint64_t nsegs = 0;
+  const uint8_t* dev_data = nullptr;  // data pointer of the last scan
+};
+
+namespace pfscdc {
+const pfscdc_params& ctx_params(const pfscdc_ctx* ctx) { return ctx->params; }
+}  // namespace pfscdc
+
+namespace {
+
+int fail(pfscdc_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_OK(ctx, expr)                                                           \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? PFSCDC_ENOMEM : PFSCDC_EHIP,   \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));               \
+  } while (0)
+
+int validate_params(const pfscdc_params* p, std::string* why) {
+  if (!p) {
+    *why = "params is NULL";
+    return PFSCDC_EINVAL;
+  }
+  if (p->average_bits < 1 || p->average_bits > 63) {
+    *why = "average_bits must be in [1, 63]";
+    return PFSCDC_EINVAL;
+  }
+  if (p->max_chunk < p->min_chunk || p->min_chunk < 1) {
+    *why = "need 1 <= min_chunk <= max_chunk";
+    return PFSCDC_EINVAL;
+  }
+  if (p->min_chunk < 64) {
+    // A cut position < 64 bytes after a reset would hash part of the zero reset window;
+    // the block-parallel scan assumes every eligible hash sees 64 real bytes.
+    *why = "min_chunk < 64 (the rolling window) is not supported on the GPU path";
+    return PFSCDC_EUNSUPPORTED;
+  }
+  return PFSCDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void pfscdc_default_params(pfscdc_params* p) {
+  p->average_bits = 23;
+  p->reserved = 0;
+  p->seed = 1;
+  p->min_chunk = 1000000;
+  p->max_chunk = 20000000;
+}
+
+int pfscdc_table(int64_t seed, uint64_t out[256]) {
+  if (!out) return PFSCDC_EINVAL;
+  generate_hashes(seed, out);
+  return PFSCDC_OK;
+}
+
+int pfscdc_go_int63(int64_t seed, int64_t* out, int n) {
+  if (!out || n < 0) return PFSCDC_EINVAL;
+  go_int63(seed, out, n);
+  return PFSCDC_OK;
+}
+
+int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out) {
+  if (!out) return PFSCDC_EINVAL;
+  *out = nullptr;
+  std::string why;
+  int rc = validate_params(params, &why);
+  if (rc) {
+    std::fprintf(stderr, "pfscdc_ctx_create: %s\n", why.c_str());
+    return rc;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    std::fprintf(stderr, "pfscdc_ctx_create: no HIP device visible\n");
+    return PFSCDC_EHIP;
+  }
+  if (device < 0 || device >= ndev) return PFSCDC_EINVAL;
+  pfscdc_ctx* c = new pfscdc_ctx();
+  c->params = *params;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return PFSCDC_EHIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  generate_hashes(params->seed, c->table);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&c->d_table, sizeof c->table) != hipSuccess ||
+      hipMemcpy(c->d_table, c->table, sizeof c->table, hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return PFSCDC_EHIP;
+  }
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return PFSCDC_EHIP;
+    }
+  c->stream = c->own_stream;
+  *out = c;
+  return PFSCDC_OK;
+}
+
+int pfscdc_ctx_destroy(pfscdc_ctx* c) {
+  if (!c) return PFSCDC_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (c->pending) (void)hipStreamSynchronize(c->stream);
+  c->d_data.release();
+  c->d_tail.release();
+  c->d_recs.release();
+  c->d_entries.release();
+  c->d_counts.release();
+  c->d_offs.release();
+  c->d_seg_base.release();
+  c->d_nseg.release();
+  c->d_seg_begin.release();
+  c->d_slots.release();
+  c->d_segs.release();
+  c->h_offs.release();
+  c->h_seg_base.release();
+  c->h_seg_begin.release();
+  c->h_segs.release();
+  if (c->d_table) (void)hipFree(c->d_table);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return PFSCDC_OK;
+}
+
+const char* pfscdc_last_error(const pfscdc_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int pfscdc_set_stream(pfscdc_ctx* c, void* hip_stream) {
+  if (!c) return PFSCDC_EINVAL;
+  c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+  return PFSCDC_OK;
+}
+
+int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                      const uint64_t* file_offsets, uint32_t nfiles) {
+  if (!c) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "previous scan not waited for");
+  if (!file_offsets) return fail(c, PFSCDC_EINVAL, "file_offsets is NULL");
+  if (nbytes && !bytes) return fail(c, PFSCDC_EINVAL, "bytes is NULL");
+  if (file_offsets[0] != 0 || file_offsets[nfiles] != nbytes)
+    return fail(c, PFSCDC_EINVAL, "file_offsets must start at 0 and end at nbytes");
+  for (uint32_t f = 0; f < nfiles; f++)
+    if (file_offsets[f + 1] < file_offsets[f])
+      return fail(c, PFSCDC_EINVAL, "file_offsets must be nondecreasing");
+  if (bytes_on_device && ((uintptr_t)bytes & 15))
+    return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const pfscdc_params& p = c->params;
+
+  // per-file segment slot ranges: every segment but a file's last is >= min bytes
+  HIP_OK(c, c->h_offs.ensure(nfiles + 1));
+  HIP_OK(c, c->h_seg_base.ensure(nfiles + 1));
+  std::memcpy(c->h_offs.p, file_offsets, sizeof(uint64_t) * (nfiles + 1));
+  uint64_t cap = 0;
+  for (uint32_t f = 0; f < nfiles; f++) {
+    c->h_seg_base.p[f] = cap;
+    const uint64_t len = file_offsets[f + 1] - file_offsets[f];
+    cap += len ? len / (uint64_t)p.min_chunk + 1 : 0;
+  }
+  c->h_seg_base.p[nfiles] = cap;
+  c->slot_cap = cap;
+  c->nfiles = nfiles;
+  c->nbytes = nbytes;
+  c->ntiles = (nbytes + kTile - 1) / kTile;
+
+  HIP_OK(c, c->d_offs.ensure(nfiles + 1));
+  HIP_OK(c, c->d_seg_base.ensure(nfiles + 1));
+  HIP_OK(c, c->d_nseg.ensure(nfiles + 1));
+  HIP_OK(c, c->d_seg_begin.ensure(nfiles + 1));
+  HIP_OK(c, c->d_slots.ensure(cap));
+  HIP_OK(c, c->d_segs.ensure(cap));
+  HIP_OK(c, c->d_recs.ensure(c->ntiles));
+  HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
+  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->d_tail.ensure(kTailBytes));
+
+  const uint8_t* data;
+  if (bytes_on_device) {
+    data = (const uint8_t*)bytes;
+  } else {
+    HIP_OK(c, c->d_data.ensure(nbytes + 64));
+    if (nbytes) HIP_OK(c, hipMemcpyAsync(c->d_data.p, bytes, nbytes, hipMemcpyHostToDevice, st));
+    data = c->d_data.p;
+  }
+  c->dev_data = data;
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (nfiles + 1),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_seg_base.p, c->h_seg_base.p, sizeof(uint64_t) * (nfiles + 1),
+                           hipMemcpyHostToDevice, st));
+  // zero-padded copy of the final partial 64-byte block (so the scan never reads past n)
+  const uint64_t n_main = nbytes & ~63ULL;
+  HIP_OK(c, hipMemsetAsync(c->d_tail.p, 0, kTailBytes, st));
+  if (nbytes > n_main)
+    HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main,
+                             hipMemcpyDeviceToDevice, st));
+  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
+
+  HIP_OK(c, hipEventRecord(c->ev[0], st));
+  if (c->ntiles) {
+    const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)2 * c->num_cus);
+    HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
+                          c->d_recs.p, grid, st));
+  }
+  HIP_OK(c, hipEventRecord(c->ev[1], st));
+  if (c->ntiles)
+    HIP_OK(c, launch_compact(c->d_recs.p, c->ntiles, nbytes, c->d_entries.p, c->d_counts.p, st));
+  HIP_OK(c, hipEventRecord(c->ev[2], st));
+  if (nfiles) {
+    HIP_OK(c, launch_select(data, c->d_table, c->d_entries.p, c->d_counts.p, c->d_offs.p,
+                            c->d_seg_base.p, nfiles, p.average_bits, (uint64_t)p.min_chunk,
+                            (uint64_t)p.max_chunk, c->d_slots.p, c->d_nseg.p, st));
+    HIP_OK(c, launch_segcompact(c->d_slots.p, c->d_seg_base.p, c->d_nseg.p, nfiles,
+                                c->d_segs.p, c->d_seg_begin.p, st));
+  }
+  HIP_OK(c, hipEventRecord(c->ev[3], st));
+  if (nfiles)
+    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap, st));
+  HIP_OK(c, hipEventRecord(c->ev[4], st));
+  HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
+  if (nfiles)
+    HIP_OK(c, hipMemcpyAsync(c->h_seg_begin.p, c->d_seg_begin.p, sizeof(uint64_t) * (nfiles + 1),
+                             hipMemcpyDeviceToHost, st));
+  else
+    c->h_seg_begin.p[0] = 0;
+  c->pending = true;
+  return PFSCDC_OK;
+}
+
+int pfscdc_wait(pfscdc_ctx* c) {
+  if (!c) return PFSCDC_EINVAL;
+  if (!c->pending) return PFSCDC_OK;
+  c->pending = false;
+  HIP_OK(c, hipSetDevice(c->device));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  const uint64_t total = c->nfiles ? c->h_seg_begin.p[c->nfiles] : 0;
+  if (total > c->slot_cap) return fail(c, PFSCDC_EHIP, "segment count exceeds slot capacity");
+  HIP_OK(c, c->h_segs.ensure(total));
+  if (total)
+    HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, total * sizeof(pfscdc_segment),
+                             hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->nsegs = total;
+  return PFSCDC_OK;
+}
+
+int pfscdc_scan(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                const uint64_t* file_offsets, uint32_t nfiles) {
+  int rc = pfscdc_scan_async(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles);
+  if (rc) return rc;
+  return pfscdc_wait(c);
+}
+
+uint64_t pfscdc_num_segments(const pfscdc_ctx* c) { return c ? c->nsegs : 0; }
+const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* c) { return c ? c->h_segs.p : nullptr; }
+const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* c) {
+  return c ? c->h_seg_begin.p : nullptr;
+}
+
+uint64_t pfscdc_debug_candidates(pfscdc_ctx* c, uint64_t* out, uint64_t cap) {
+  if (!c || c->pending || !c->ntiles) return 0;
+  uint64_t ne = 0;
+  if (hipMemcpy(&ne, c->d_counts.p, sizeof ne, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (out && cap) {
+    const uint64_t k = std::min(ne, cap);
+    if (hipMemcpy(out, c->d_entries.p, k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+      return 0;
+  }
+  return ne;
+}
+
+int pfscdc_last_timings(pfscdc_ctx* c, float out[5]) {
+  if (!c || !out) return PFSCDC_EINVAL;
+  HIP_OK(c, hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]));
+  HIP_OK(c, hipEventElapsedTime(&out[1], c->ev[1], c->ev[2]));
+  HIP_OK(c, hipEventElapsedTime(&out[2], c->ev[2], c->ev[3]));
+  HIP_OK(c, hipEventElapsedTime(&out[3], c->ev[3], c->ev[4]));
+  HIP_OK(c, hipEventElapsedTime(&out[4], c->ev[0], c->ev[4]));
+  return PFSCDC_OK;
+}
+
+void* pfscdc_host_alloc(uint64_t nbytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, nbytes ? nbytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void pfscdc_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
+                          uint32_t nfiles, uint64_t seed) {
+  if (!c || !file_offsets || (!dev_bytes && nfiles && file_offsets[nfiles])) return PFSCDC_EINVAL;
+  if (nfiles == 0 || file_offsets[nfiles] == 0) return PFSCDC_OK;
+  HIP_OK(c, hipSetDevice(c->device));
+  HIP_OK(c, c->h_offs.ensure(nfiles + 1));
+  HIP_OK(c, c->d_offs.ensure(nfiles + 1));
+  std::memcpy(c->h_offs.p, file_offsets, sizeof(uint64_t) * (nfiles + 1));
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (nfiles + 1),
+                           hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, launch_synth((uint8_t*)dev_bytes, c->d_offs.p, nfiles, seed, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return PFSCDC_OK;
+}
+
+}  // extern "C"

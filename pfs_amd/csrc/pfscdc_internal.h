@@ -1,0 +1,53 @@
+// pfscdc_internal.h — shared constants and launcher declarations (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pfscdc.h"
+
+namespace pfscdc {
+
+// candidate scan geometry: 512 lanes x 4 KiB strips = 2 MiB tile per workgroup iteration
+constexpr int kScanBlock = 512;
+constexpr int kStrip = 4096;
+constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
+constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
+constexpr int kTileCandCap = 64;    // LDS staging per tile
+constexpr uint32_t kTableLdsBytes = 256u * 256u;  // T x 32 bank-disjoint copies
+constexpr int kCompactBlock = 1024;
+constexpr int kSelectBlock = 256;   // 4 files (waves) per block
+constexpr int kHashBlock = 256;     // 64 segments per block
+constexpr uint64_t kDenseBit = 1ULL << 63;
+constexpr uint64_t kNone = ~0ULL;
+constexpr uint64_t kTailBytes = 256;  // zero-padded copy of the final partial 64-byte block
+
+struct TileRec {
+  uint32_t count;
+  uint32_t off[kTileK];
+};
+static_assert(sizeof(TileRec) == 64, "tile record is one 64-byte line");
+static_assert(sizeof(pfscdc_segment) == 56, "segment record layout");
+
+void generate_hashes(int64_t seed, uint64_t out[256]);
+const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
+void go_int63(int64_t seed, int64_t* out, int n);
+
+hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
+                       uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
+                       hipStream_t st);
+hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
+                          uint64_t* n_entries, hipStream_t st);
+hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,
+                         const uint64_t* n_entries, const uint64_t* offs,
+                         const uint64_t* seg_base, uint32_t nfiles, uint32_t average_bits,
+                         uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
+                         uint64_t* nseg, hipStream_t st);
+hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_base,
+                             const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
+                             uint64_t* seg_begin, hipStream_t st);
+hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
+                          const uint64_t* seg_count, uint64_t max_segments, hipStream_t st);
+hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
+                        hipStream_t st);
+
+}  // namespace pfscdc

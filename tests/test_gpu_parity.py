@@ -1,0 +1,177 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle on the same bytes.
+
+Bar: bit-exact — every segment offset/size/cut flag and every BLAKE2b-256 digest equal to
+the restated reference chunker (oracle/cdc_oracle.c, itself cross-checked against the
+literal Python Writer and hashlib in the CPU suite).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import chunker as Ch
+from oracle import coracle
+from pfs_amd import _lib
+from pfs_amd.cdc import ChunkParams, Chunker, synthetic_bytes
+
+pytestmark = pytest.mark.gpu
+
+SMALL = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+DEFAULT = Ch.Params()
+
+
+def cp(p: Ch.Params) -> ChunkParams:
+    return ChunkParams(p.average_bits, p.seed, p.min, p.max)
+
+
+_CHUNKERS = {}
+
+
+def chunker_for(p: Ch.Params) -> Chunker:
+    if p not in _CHUNKERS:
+        _CHUNKERS[p] = Chunker(cp(p), device=0)
+    return _CHUNKERS[p]
+
+
+def assert_same(gpu_res, data, offs, p, nthreads=8):
+    segs, begin = coracle.segment_files(data, offs, p, nthreads=nthreads)
+    g = gpu_res.segments
+    assert np.array_equal(gpu_res.file_begin, begin), "per-file segment counts differ"
+    assert len(g) == len(segs)
+    for field in ("offset", "size", "file", "flags"):
+        bad = np.nonzero(g[field] != segs[field])[0]
+        assert len(bad) == 0, f"{field} differs at segments {bad[:5]}: gpu={g[bad[:5]]} cpu={segs[bad[:5]]}"
+    bad = np.nonzero((g["hash"] != segs["hash"]).any(axis=1))[0]
+    assert len(bad) == 0, f"digests differ at segments {bad[:5]}"
+
+
+def random_offsets(rng, nfiles, max_len):
+    lens = rng.integers(0, max_len, nfiles)
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_small_params_many_files(seed):
+    rng = np.random.default_rng(seed)
+    offs = random_offsets(rng, 300, 120_000)
+    data = synthetic_bytes(offs, seed)
+    assert_same(chunker_for(SMALL).scan(data, offs), data, offs, SMALL)
+
+
+def test_default_params_multi_mib():
+    offs = np.array([0, 3 << 20, (3 << 20) + 12345, (3 << 20) + 12345 + (9 << 20) + 7,
+                     (13 << 20) + 999_999, (13 << 20) + 2_000_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 11)
+    assert_same(chunker_for(DEFAULT).scan(data, offs), data, offs, DEFAULT)
+
+
+def test_default_params_long_stream_forces_max():
+    # 64 MiB single stream: candidates every ~8 MiB and some 20 MB forced cuts
+    offs = np.array([0, 64 << 20], dtype=np.uint64)
+    data = synthetic_bytes(offs, 0xC1)
+    res = chunker_for(DEFAULT).scan(data, offs)
+    assert_same(res, data, offs, DEFAULT)
+    assert len(res.segments) >= 4
+
+
+def test_edge_sizes():
+    p = SMALL
+    lens = [0, 1, 63, 64, 65, 127, 128, 129, 1999, 2000, 2001, 29999, 30000, 30001, 0, 0,
+            60000, 60001, 4096, 12345, 0]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 5)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
+def test_empty_batches():
+    c = chunker_for(SMALL)
+    r = c.scan(b"", [0])
+    assert len(r.segments) == 0
+    r = c.scan(b"", [0, 0, 0])
+    assert len(r.segments) == 0 and list(r.file_begin) == [0, 0, 0]
+
+
+def test_dense_candidates_rescan_path():
+    # average_bits=4 makes ~1/16 of positions candidates: every tile overflows its 15 slots
+    p = Ch.Params(average_bits=4, seed=1, min=100, max=5000)
+    rng = np.random.default_rng(9)
+    offs = random_offsets(rng, 40, 300_000)
+    data = synthetic_bytes(offs, 9)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
+def test_periodic_data_dense_then_sparse():
+    # locally dense tiles (repeating 48-byte pattern) next to random bytes
+    p = Ch.Params(average_bits=10, seed=1, min=3000, max=40000)
+    pat = np.frombuffer(bytes(range(48)), dtype=np.uint8)
+    rnd = synthetic_bytes([0, 3 << 20], 4)
+    blocks = []
+    for i in range(6):
+        blocks.append(np.tile(pat, (1 << 20) // 48 + 1)[: (1 << 20) + 17 * i])
+        blocks.append(rnd[i << 19:(i + 1) << 19])
+    data = np.concatenate(blocks)
+    offs = np.array([0, len(data) // 3, len(data)], dtype=np.uint64)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
+def test_wide_mask():
+    p = Ch.Params(average_bits=33, seed=3, min=1000, max=9000)
+    offs = np.array([0, 500_000, 500_001, 900_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 3)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
+def test_index_writer_seed0_avgbits20():
+    # fileset/index/writer.go:60 uses WithRollingHashConfig(20, 0) (then level+1 seeds)
+    for seed in (0, 1, 2):
+        p = Ch.Params(average_bits=20, seed=seed, min=1_000_000, max=20_000_000)
+        offs = np.array([0, 5 << 20, (5 << 20) + 4_000_000], dtype=np.uint64)
+        data = synthetic_bytes(offs, 100 + seed)
+        assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
+def test_candidate_list_matches_oracle():
+    # ~2 candidates per 2 MiB tile: every tile stays sparse (<= 15 stored candidates)
+    p = Ch.Params(average_bits=20, seed=1, min=2000, max=30000)
+    n = (9 << 20) + 77
+    data = synthetic_bytes([0, n], 21)
+    c = chunker_for(p)
+    c.scan(data, [0, n])
+    gpu = c.debug_candidates()
+    assert not np.any(gpu >> np.uint64(63)), "unexpected dense tile"
+    cpu = coracle.candidates(data, p)
+    assert np.array_equal(gpu, cpu)
+
+
+def test_device_resident_input_matches_host_input():
+    import torch
+
+    p = DEFAULT
+    offs = np.array([0] + [(i + 1) * (4 << 20) for i in range(16)], dtype=np.uint64)
+    c = chunker_for(p)
+    dev = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c.fill_synthetic(dev, offs, 0xC2)
+    host = synthetic_bytes(offs, 0xC2)
+    assert np.array_equal(dev.cpu().numpy(), host), "device synthetic generator differs"
+    r_dev = c.scan(dev, offs)
+    assert_same(r_dev, host, offs, p)
+
+
+def test_unaligned_device_pointer_rejected():
+    import torch
+
+    c = chunker_for(SMALL)
+    dev = torch.zeros(1000, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(_lib.PfsCdcError):
+        c.scan(dev[1:], [0, 999])
+
+
+def test_digests_are_blake2b_of_segment_bytes():
+    p = SMALL
+    offs = np.array([0, 70_000, 70_000 + 33_333], dtype=np.uint64)
+    data = synthetic_bytes(offs, 2)
+    r = chunker_for(p).scan(data, offs)
+    for s in r.segments:
+        a = int(offs[s["file"]] + s["offset"])
+        want = hashlib.blake2b(data[a:a + int(s["size"])].tobytes(), digest_size=32).digest()
+        assert bytes(s["hash"]) == want
