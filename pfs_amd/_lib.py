@@ -98,6 +98,14 @@ def load() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `make` or "
                               "`python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: PyTorch wheels ship their own libamdhip64.so.7 (same
+        # SONAME as /opt/rocm's).  Importing torch first makes the dynamic linker bind
+        # libpfscdc.so to torch's copy, so device pointers, streams and the device context
+        # are shared; loading ours first would leave torch unable to see the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         u64, i64, u32, i32, vp = C.c_uint64, C.c_int64, C.c_uint32, C.c_int, C.c_void_p
         P = C.POINTER

@@ -134,34 +134,40 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
   }
 }
 
-// One 64-byte block: prefetch the block after it into NXT, roll IN against OUT (the block
-// 64 bytes earlier supplies the outgoing bytes), test all 64 positions with one min-reduce.
-#define PFS_SCAN_BLOCK(IN, OUT, NXT)                                                     \
-  {                                                                                      \
-    if (pos >= s1) break;                                                                \
-    load64(NXT, block_src(data, tail, n_main, pos + 64));                                \
-    const uint32_t hl0 = hl, hh0 = hh;                                                   \
-    uint32_t acc = 0xffffffffu;                                                          \
-    _Pragma("unroll") for (int t = 0; t < 64; t++) {                                     \
-      PFS_ROLL(IN[t >> 2], OUT[t >> 2], t & 3);                                          \
-      const uint32_t key = cand_key<WIDE>(hl, hh, kshift);                               \
-      acc = acc < key ? acc : key;                                                       \
-    }                                                                                    \
-    if (__builtin_expect(acc == 0, 0))                                                   \
-      record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, pos, n, tile_base,  \
-                   mask64, table, s_count, s_cand);                                      \
-    pos += 64;                                                                           \
+// Roll 64 positions: IN = this block's 16 dwords, OUT = the block 64 bytes earlier; test all
+// 64 positions with one min-reduce and fall into the exact re-roll only if one hit.
+#define PFS_ROLL64(IN, OUT, POS)                                                          \
+  {                                                                                       \
+    const uint32_t hl0 = hl, hh0 = hh;                                                    \
+    uint32_t acc = 0xffffffffu;                                                           \
+    _Pragma("unroll") for (int t = 0; t < 64; t++) {                                      \
+      PFS_ROLL(IN[t >> 2], OUT[t >> 2], t & 3);                                           \
+      const uint32_t key = cand_key<WIDE>(hl, hh, kshift);                                \
+      acc = acc < key ? acc : key;                                                        \
+    }                                                                                     \
+    if (__builtin_expect(acc == 0, 0))                                                    \
+      record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, (POS), n, tile_base,  \
+                   mask64, table, s_count, s_cand);                                       \
   }
 
+// Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
+// them 128 bytes at a time.  Per step, 8 LDS-DMA instructions (global_load_lds_dwordx4)
+// each fetch one full 128-byte line from 8 strips (8 lines per instruction: the coalesced
+// rate; per-lane strip loads touch 64 lines per instruction and run at ~2.1 TB/s), into a
+// per-wave 8 KiB LDS image of 64 rows x 128 B.  Chunk c of row r sits in slot c ^ swz(r),
+// swz(r) = (r >> 1) & 7, so the row reads (ds_read_b128) are bank-conflict free.
+PFS_DEV uint32_t stage_swz(uint32_t r) { return (r >> 1) & 7u; }
+
 template <bool WIDE>
-__global__ __launch_bounds__(kScanBlock, 4) void cdc_scan_kernel(
+__global__ __launch_bounds__(kScanBlock) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs) {
-  // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then count + candidates.
+  // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
+  // images, then the tile's candidate count + list.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* s_count = reinterpret_cast<uint32_t*>(smem + kTableLdsBytes);
-  uint32_t* s_cand = reinterpret_cast<uint32_t*>(smem + kTableLdsBytes + 16);
+  uint32_t* s_count = reinterpret_cast<uint32_t*>(smem + kScanCandLds);
+  uint32_t* s_cand = s_count + 4;
   const uint64_t n_main = n & ~63ULL;
 
   // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
@@ -169,38 +175,79 @@ __global__ __launch_bounds__(kScanBlock, 4) void cdc_scan_kernel(
     const int idx = i >> 5, c = i & 31;
     reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] = table[idx];
   }
-  const uint32_t lane_off = (threadIdx.x & 31u) * 8u;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lane_off = (lane & 31u) * 8u;
+  uint8_t* wbuf = smem + kTableLdsBytes + wave * kStageBytes;
+  const uint32_t rd_base = lane * 128u;
+  const uint32_t swz_l = stage_swz(lane);
+  // this lane's DMA piece in instruction i: row r_i = 8i + lane/8, chunk (lane%8) ^ swz(r_i)
+  uint32_t dma_off[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t r = 8u * i + (lane >> 3);
+    dma_off[i] = r * kStrip + 16u * ((lane & 7u) ^ stage_swz(r));
+  }
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     if (threadIdx.x == 0) *s_count = 0;
     __syncthreads();
     const uint64_t tile_base = tile * kTile;
-    const uint64_t s0 = tile_base + (uint64_t)threadIdx.x * kStrip;
-    if (s0 < n) {
-      const uint64_t s1 = (s0 + kStrip < n) ? s0 + kStrip : n;
-      uint32_t b0[16], b1[16], b2[16];
-      if (s0 >= 64) {
-        load64(b2, block_src(data, tail, n_main, s0 - 64));
+    const uint64_t wave_base = tile_base + (uint64_t)wave * 64 * kStrip;
+    if (wave_base < n) {  // wave-uniform
+      const bool fast = wave_base + 64 * (uint64_t)kStrip <= n_main;
+      auto dma_step = [&](uint32_t step) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint64_t p = wave_base + dma_off[i] + step * 128u;
+          const uint8_t* src = (fast || p < n_main) ? data + p
+                               : tail + (p - n_main < 64 ? p - n_main : 64);
+          __builtin_amdgcn_global_load_lds((const void*)src,
+              (__attribute__((address_space(3))) void*)(wbuf + i * 1024), 16, 0, 0);
+        }
+      };
+      const uint64_t s0 = wave_base + (uint64_t)lane * kStrip;
+      dma_step(0);
+      uint32_t prv[16], cur[32];
+      if (s0 >= 64 && s0 - 64 < n) {
+        load64(prv, block_src(data, tail, n_main, s0 - 64));
       } else {
 #pragma unroll
-        for (int i = 0; i < 16; i++) b2[i] = 0;  // reset window (writer.go:17-19)
+        for (int i = 0; i < 16; i++) prv[i] = 0;  // reset window (writer.go:17-19)
       }
-      load64(b0, block_src(data, tail, n_main, s0));
       // Write(window): h = XOR rotl(T[b_j], 63 - j) == h_{s0-1}
       uint32_t hl = 0, hh = 0;
 #pragma unroll
       for (int t = 0; t < 64; t++) {
-        const uint64_t ti = lds_abs_u64(tab_addr(b2[t >> 2], lane_off, t & 3));
+        const uint64_t ti = lds_abs_u64(tab_addr(prv[t >> 2], lane_off, t & 3));
         const uint32_t nl = __builtin_amdgcn_alignbit(hl, hh, 31);
         const uint32_t nh = __builtin_amdgcn_alignbit(hh, hl, 31);
         hl = nl ^ (uint32_t)ti;
         hh = nh ^ (uint32_t)(ti >> 32);
       }
-      uint64_t pos = s0;
-      while (true) {
-        PFS_SCAN_BLOCK(b0, b2, b1)
-        PFS_SCAN_BLOCK(b1, b0, b2)
-        PFS_SCAN_BLOCK(b2, b1, b0)
+      const bool active = s0 < n;
+      for (uint32_t step = 0; step < kStrip / 128; step++) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's DMA has landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+          const uint4 v = *reinterpret_cast<const uint4*>(wbuf + rd_base + 16u * (c ^ swz_l));
+          cur[4 * c + 0] = v.x;
+          cur[4 * c + 1] = v.y;
+          cur[4 * c + 2] = v.z;
+          cur[4 * c + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row is in registers
+        __builtin_amdgcn_wave_barrier();
+        if (step + 1 < kStrip / 128) dma_step(step + 1);    // refill while we compute
+        const uint64_t pos = s0 + step * 128u;
+        if (active && pos < n) {
+          uint32_t* c0 = cur;
+          uint32_t* c1 = cur + 16;
+          PFS_ROLL64(c0, prv, pos)
+          if (pos + 64 < n) PFS_ROLL64(c1, c0, pos + 64)
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) prv[i] = cur[16 + i];
       }
     }
     __syncthreads();
@@ -435,25 +482,40 @@ __constant__ uint32_t kSigmaPack[12][4] = {
 #undef PK
 };
 
-PFS_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotations on register halves (v_alignbit_b32 x2; rotr 32 is a register swap).
+PFS_DEV uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+PFS_DEV uint64_t xor_rotr32(uint64_t x, uint64_t y) {
+  return mk64((uint32_t)(x >> 32) ^ (uint32_t)(y >> 32), (uint32_t)x ^ (uint32_t)y);
+}
+template <int N>
+PFS_DEV uint64_t xor_rotr(uint64_t x, uint64_t y) {  // rotr64(x ^ y, N), 0 < N < 32
+  const uint32_t lo = (uint32_t)x ^ (uint32_t)y, hi = (uint32_t)(x >> 32) ^ (uint32_t)(y >> 32);
+  return mk64(__builtin_amdgcn_alignbit(hi, lo, N), __builtin_amdgcn_alignbit(lo, hi, N));
+}
+PFS_DEV uint64_t xor_rotr63(uint64_t x, uint64_t y) {  // rotr64(x ^ y, 63) = rotl 1
+  const uint32_t lo = (uint32_t)x ^ (uint32_t)y, hi = (uint32_t)(x >> 32) ^ (uint32_t)(y >> 32);
+  return mk64(__builtin_amdgcn_alignbit(lo, hi, 31), __builtin_amdgcn_alignbit(hi, lo, 31));
+}
 
 template <int CTRL>
 PFS_DEV uint64_t quad_perm64(uint64_t x) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, true);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
-  return ((uint64_t)hi << 32) | lo;
+  return mk64(lo, hi);
 }
 
+// BLAKE2b G (RFC 7693 §3.1) on one column held by this lane: 6 v_lshl_add_u64,
+// 8 v_xor_b32, 6 v_alignbit_b32.
 #define PFS_G(a, b, c, d, x, y)  \
   do {                           \
     a = a + b + (x);             \
-    d = rotr64(d ^ a, 32);       \
+    d = xor_rotr32(d, a);        \
     c = c + d;                   \
-    b = rotr64(b ^ c, 24);       \
+    b = xor_rotr<24>(b, c);      \
     a = a + b + (y);             \
-    d = rotr64(d ^ a, 16);       \
+    d = xor_rotr<16>(d, a);      \
     c = c + d;                   \
-    b = rotr64(b ^ c, 63);       \
+    b = xor_rotr63(b, c);        \
   } while (0)
 
 // Lane q of the quad loads bytes [32q, 32q+32) of a 128-byte message block.
@@ -462,13 +524,18 @@ PFS_DEV void msg_load_full(uint4& m0, uint4& m1, const uint8_t* p) {
   __builtin_memcpy(&m1, p + 16, 16);
 }
 
+// Last block of a segment: bytes at or past `avail` are zero (BLAKE2b pads with zeros).
 PFS_DEV void msg_load_tail(uint4& m0, uint4& m1, const uint8_t* p, int64_t avail) {
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     uint32_t v = 0;
-    for (int b = 0; b < 4; b++)
-      if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
+    if (4 * i + 4 <= avail) {
+      __builtin_memcpy(&v, p + 4 * i, 4);
+    } else {
+      for (int b = 0; b < 4; b++)
+        if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
+    }
     w[i] = v;
   }
   m0 = make_uint4(w[0], w[1], w[2], w[3]);
@@ -488,9 +555,14 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   const uint32_t slot = (threadIdx.x >> 2) * 256u;  // low byte 0: perm builds the address
   uint8_t* my = s_msg + slot + 32u * j;
 
-  uint32_t pk[12];
+  // LDS addresses of the 4 message words this lane consumes in each round (loop invariant)
+  uint32_t ma[12][4];
 #pragma unroll
-  for (int r = 0; r < 12; r++) pk[r] = kSigmaPack[r][j];
+  for (int r = 0; r < 12; r++) {
+    const uint32_t pk = kSigmaPack[r][j];
+#pragma unroll
+    for (int k = 0; k < 4; k++) ma[r][k] = __builtin_amdgcn_perm(pk, slot, 0x0c0c0104u + k);
+  }
 
   const uint64_t iv_c = kB2IV[j];
   const uint64_t iv_d = kB2IV[4 + j];
@@ -509,6 +581,9 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // software pipeline: round 0's message words, then each round fetches the next one's
+    uint64_t x0 = lds_load<uint64_t>(s_msg, ma[0][0]), x1 = lds_load<uint64_t>(s_msg, ma[0][1]);
+    uint64_t x2 = lds_load<uint64_t>(s_msg, ma[0][2]), x3 = lds_load<uint64_t>(s_msg, ma[0][3]);
     if (!last) {  // prefetch the next block into registers while this one compresses
       const uint64_t nb = blk + 1;
       const uint8_t* p = src + nb * 128 + 32 * j;
@@ -520,19 +595,22 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     uint64_t d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
 #pragma unroll
     for (int r = 0; r < 12; r++) {
-      const uint32_t base = slot;
-      const uint64_t x0 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0104u));
-      const uint64_t x1 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0105u));
-      const uint64_t x2 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0106u));
-      const uint64_t x3 = lds_load<uint64_t>(s_msg, __builtin_amdgcn_perm(pk[r], base, 0x0c0c0107u));
+      uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+      if (r < 11) {
+        y0 = lds_load<uint64_t>(s_msg, ma[r + 1][0]);
+        y1 = lds_load<uint64_t>(s_msg, ma[r + 1][1]);
+        y2 = lds_load<uint64_t>(s_msg, ma[r + 1][2]);
+        y3 = lds_load<uint64_t>(s_msg, ma[r + 1][3]);
+      }
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
-      b = quad_perm64<0x39>(b);            // b <- v[4+(j+1)%4]
       c = quad_perm64<0x4E>(c);            // c <- v[8+(j+2)%4]
       d = quad_perm64<0x93>(d);            // d <- v[12+(j+3)%4]
+      b = quad_perm64<0x39>(b);            // b <- v[4+(j+1)%4]
       PFS_G(a, b, c, d, x2, x3);           // diagonal step: G_{4+j}
-      b = quad_perm64<0x93>(b);
       c = quad_perm64<0x4E>(c);
       d = quad_perm64<0x39>(d);
+      b = quad_perm64<0x93>(b);
+      x0 = y0; x1 = y1; x2 = y2; x3 = y3;
     }
     ha ^= a ^ c;
     hb ^= b ^ d;
@@ -590,7 +668,7 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        hipStream_t st) {
-  const size_t lds = kTableLdsBytes + 16 + 4 * kTileCandCap;
+  const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   if (average_bits <= 32) {
     static bool attr = false;

@@ -14,6 +14,10 @@ constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
 constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
 constexpr int kTileCandCap = 64;    // LDS staging per tile
 constexpr uint32_t kTableLdsBytes = 256u * 256u;  // T x 32 bank-disjoint copies
+constexpr uint32_t kStageBytes = 64u * 128u;       // per-wave LDS-DMA image: 64 rows x 128 B
+constexpr uint32_t kScanCandLds = kTableLdsBytes + (kScanBlock / 64) * kStageBytes;
+constexpr uint32_t kScanLdsBytes = kScanCandLds + 16 + 4 * kTileCandCap;
+static_assert(kScanLdsBytes <= 160 * 1024, "scan kernel LDS budget");
 constexpr int kCompactBlock = 1024;
 constexpr int kSelectBlock = 256;   // 4 files (waves) per block
 constexpr int kHashBlock = 256;     // 64 segments per block
