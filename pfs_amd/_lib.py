@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpfscdc.so")
+LIB_PATH = os.environ.get("PFSCDC_LIB") or os.path.join(_HERE, "libpfscdc.so")  # env: A/B builds
 
 PFSCDC_OK = 0
 PFSCDC_EINVAL = -1

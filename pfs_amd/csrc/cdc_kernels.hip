@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pfscdc_internal.h"
 
 #define PFS_DEV __device__ __forceinline__
@@ -37,7 +39,11 @@ PFS_DEV uint64_t rotl1_64(uint64_t x) { return (x << 1) | (x >> 63); }
 
 // LDS byte address of T[byte j of w] in this lane's copy: (idx << 8) | (lane & 31) * 8.
 PFS_DEV uint32_t tab_addr(uint32_t w, uint32_t lane_off, int j) {
+#ifdef PFS_EXP_NO_PERM
+  return __builtin_amdgcn_bitop3_b32(w, 0xFF00u, lane_off, 0xEC);  // (w & m) | l (timing only)
+#else
   return __builtin_amdgcn_perm(w, lane_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
+#endif
 }
 
 template <typename T>
@@ -52,9 +58,7 @@ PFS_DEV uint64_t lds_abs_u64(uint32_t a) { return *(lds_u64_t*)(uintptr_t)a; }
 
 // gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is a 3-input XOR.
 PFS_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t d;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -136,15 +140,74 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
 
 // Roll 64 positions: IN = this block's 16 dwords, OUT = the block 64 bytes earlier; test all
 // 64 positions with one min-reduce and fall into the exact re-roll only if one hit.
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, I1).
+template <int I, int I1>
+struct StaticFor {
+  template <class F>
+  static PFS_DEV void run(F&& f) {
+    if constexpr (I < I1) {
+      f(std::integral_constant<int, I>{});
+      StaticFor<I + 1, I1>::run(f);
+    }
+  }
+};
+
+// T lookup issued by hand so the waits can be counted exactly (the compiler falls back to
+// lgkmcnt(0) around LDS-DMA); consumers sit behind an explicit s_waitcnt + sched_barrier.
+PFS_DEV uint64_t lds_read_async(uint32_t a) {
+  uint64_t v;
+#ifdef PFS_EXP_NO_TABLE
+  v = ((uint64_t)(a ^ 0x7F4A7C15u) << 32) | (a ^ 0xC2B2AE35u);
+#else
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+#endif
+  return v;
+}
+
+#ifndef PFS_EXP_AHEAD
+#define PFS_EXP_AHEAD 8
+#endif
+static_assert(PFS_EXP_AHEAD >= 1 && 2 * (PFS_EXP_AHEAD - 1) <= 15, "lgkmcnt is 4 bits");
+constexpr int kRollAhead = PFS_EXP_AHEAD;
+#ifdef PFS_EXP_NO_ROT
+#define PFS_ROT1(NL, NH) const uint32_t NL = hh, NH = hl;  /* timing only */
+#else
+#define PFS_ROT1(NL, NH)                                   \
+  const uint32_t NL = __builtin_amdgcn_alignbit(hl, hh, 31); \
+  const uint32_t NH = __builtin_amdgcn_alignbit(hh, hl, 31);
+#endif  // bytes of T lookups in flight (2 ds_read_b64 each; lgkmcnt <= 15)
+
+// Roll 64 positions: IN = this block's 16 dwords, OUT = the block 64 bytes earlier; test all
+// 64 positions with one min-reduce and fall into the exact re-roll only if one hit.
 #define PFS_ROLL64(IN, OUT, POS)                                                          \
   {                                                                                       \
     const uint32_t hl0 = hl, hh0 = hh;                                                    \
     uint32_t acc = 0xffffffffu;                                                           \
-    _Pragma("unroll") for (int t = 0; t < 64; t++) {                                      \
-      PFS_ROLL(IN[t >> 2], OUT[t >> 2], t & 3);                                           \
+    uint64_t ti_[kRollAhead], to_[kRollAhead];                                            \
+    StaticFor<0, kRollAhead>::run([&](auto tc) {                                          \
+      constexpr int t = decltype(tc)::value;                                              \
+      ti_[t] = lds_read_async(tab_addr(IN[t >> 2], lane_off, t & 3));                     \
+      to_[t] = lds_read_async(tab_addr(OUT[t >> 2], lane_off, t & 3));                    \
+    });                                                                                   \
+    StaticFor<0, 64>::run([&](auto tc) {                                                  \
+      constexpr int t = decltype(tc)::value;                                              \
+      /* pairs in flight: t .. min(t+K-1, 63); wait until only the younger ones remain */  \
+      constexpr int inflight = (64 - t < kRollAhead) ? 64 - t : kRollAhead;               \
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (inflight - 1)) << 8));                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      const uint64_t a_ = ti_[t % kRollAhead], b_ = to_[t % kRollAhead];                  \
+      PFS_ROT1(nl_, nh_)                                                                  \
+      hl = xor3(nl_, (uint32_t)a_, (uint32_t)b_);                                         \
+      hh = xor3(nh_, (uint32_t)(a_ >> 32), (uint32_t)(b_ >> 32));                         \
       const uint32_t key = cand_key<WIDE>(hl, hh, kshift);                                \
       acc = acc < key ? acc : key;                                                        \
-    }                                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr (t + kRollAhead < 64) {                                                \
+        constexpr int u = t + kRollAhead;                                                 \
+        ti_[t % kRollAhead] = lds_read_async(tab_addr(IN[u >> 2], lane_off, u & 3));      \
+        to_[t % kRollAhead] = lds_read_async(tab_addr(OUT[u >> 2], lane_off, u & 3));     \
+      }                                                                                   \
+    });                                                                                   \
     if (__builtin_expect(acc == 0, 0))                                                    \
       record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, (POS), n, tile_base,  \
                    mask64, table, s_count, s_cand);                                       \
@@ -159,7 +222,7 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
 PFS_DEV uint32_t stage_swz(uint32_t r) { return (r >> 1) & 7u; }
 
 template <bool WIDE>
-__global__ __launch_bounds__(kScanBlock) void cdc_scan_kernel(
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs) {
@@ -226,7 +289,9 @@ __global__ __launch_bounds__(kScanBlock) void cdc_scan_kernel(
       }
       const bool active = s0 < n;
       for (uint32_t step = 0; step < kStrip / 128; step++) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's DMA has landed
+#ifndef PFS_EXP_NO_DMA_WAIT
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's DMA has landed
+#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int c = 0; c < 8; c++) {
@@ -236,7 +301,7 @@ __global__ __launch_bounds__(kScanBlock) void cdc_scan_kernel(
           cur[4 * c + 2] = v.z;
           cur[4 * c + 3] = v.w;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row is in registers
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): row is in registers (WAR vs DMA)
         __builtin_amdgcn_wave_barrier();
         if (step + 1 < kStrip / 128) dma_step(step + 1);    // refill while we compute
         const uint64_t pos = s0 + step * 128u;

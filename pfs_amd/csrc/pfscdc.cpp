@@ -297,7 +297,7 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
   if (c->ntiles) {
-    const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)2 * c->num_cus);
+    const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
                           c->d_recs.p, grid, st));
   }

@@ -108,6 +108,89 @@ __global__ void rd_strip(const uint8_t* __restrict__ p, uint64_t n, uint32_t* ou
   if (acc == 0x1234567) out[0] = acc;
 }
 
+// Does a pending LDS-DMA (global_load_lds) count in lgkmcnt?  t[0]: ds_read + lgkmcnt(0);
+// t[1]: DMA then ds_read + lgkmcnt(0); t[2]: DMA then vmcnt(0).
+__global__ void dma_lgkm(const uint8_t* __restrict__ src, uint64_t* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[4096];
+  const int lane = threadIdx.x & 63;
+  buf[lane] = lane; __syncthreads();
+  uint32_t v = 0;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  t0 = __builtin_amdgcn_s_memtime();
+  asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lane * 4) : "memory");
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  uint64_t t2 = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16), (__attribute__((address_space(3))) void*)(buf + 1024), 16, 0, 0);
+  asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lane * 4) : "memory");
+  uint64_t t3 = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  uint64_t t4 = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_global_load_lds((const void*)(src + 65536 + lane * 16), (__attribute__((address_space(3))) void*)(buf + 2048), 16, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint64_t t5 = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = t3 - t2; out[2] = t5 - t4; out[3] = v; }
+}
+
+// Aggregate VALU throughput: every wave runs 8 independent chains; result = instructions
+// issued per SIMD per cycle (all waves) using the slowest wave's s_memtime span.
+template <int K> __global__ void thr(uint64_t* out, uint32_t seed) {
+  if constexpr (K == 16) {  // 64-bit ops
+    uint64_t x0 = seed + threadIdx.x, x1 = x0 * 3, x2 = x0 ^ 5, x3 = x0 + 9, y = seed * 17ull + 1;
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < 256; r++)
+      asm volatile(".rept 8\nv_lshl_add_u64 %0, %0, 1, %4\nv_lshl_add_u64 %1, %1, 1, %4\nv_lshl_add_u64 %2, %2, 1, %4\nv_lshl_add_u64 %3, %3, 1, %4\n.endr" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "v"(y));
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) out[blockIdx.x * 32 + (threadIdx.x >> 6)] = t1 - t0;
+    if ((x0 ^ x1 ^ x2 ^ x3) == 0x1234567) out[100000] = 1;
+    return;
+  }
+  uint32_t a0 = seed + threadIdx.x, a1 = a0 * 3, a2 = a0 ^ 5, a3 = a0 + 9, a4 = a0 * 7, a5 = a0 ^ 77, a6 = a0 + 1234, a7 = a0 * 13;
+  uint32_t b = seed * 17 + 1, c = seed ^ 0x99;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < 256; r++) {
+#define CH8(OP) asm volatile(".rept 4\n" OP("%0") OP("%1") OP("%2") OP("%3") OP("%4") OP("%5") OP("%6") OP("%7") ".endr\n" \
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "v"(c));
+#define XOR(R) "v_xor_b32 " R ", " R ", %8\n"
+#define ALB(R) "v_alignbit_b32 " R ", " R ", %8, 31\n"
+#define B3(R) "v_bitop3_b32 " R ", " R ", %8, %9 bitop3:0x96\n"
+#define PRM(R) "v_perm_b32 " R ", " R ", %8, %9\n"
+#define ANDOR(R) "v_and_or_b32 " R ", " R ", %8, %9\n"
+#define LSHLOR(R) "v_lshl_or_b32 " R ", " R ", 1, %9\n"
+#define OR3(R) "v_or3_b32 " R ", " R ", %8, %9\n"
+#define BFE(R) "v_bfe_u32 " R ", " R ", 8, 8\n"
+#define LSHL(R) "v_lshlrev_b32 " R ", 1, " R "\n"
+#define SDWA(R) "v_lshlrev_b32_sdwa " R ", 8, " R " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+#define MIN3(R) "v_min3_u32 " R ", " R ", %8, %9\n"
+#define MIN(R) "v_min_u32 " R ", " R ", %8\n"
+#define MAD24(R) "v_mad_u32_u24 " R ", " R ", %8, %9\n"
+#define ADD3(R) "v_add3_u32 " R ", " R ", %8, %9\n"
+#define XDPP(R) "v_xor_b32_dpp " R ", %8, " R " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+#define LSHLORDPP(R) "v_or_b32_sdwa " R ", %8, " R " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD\n"
+    if (K == 0) CH8(XOR)
+    if (K == 1) CH8(ALB)
+    if (K == 2) CH8(B3)
+    if (K == 3) CH8(PRM)
+    if (K == 4) CH8(ANDOR)
+    if (K == 5) CH8(LSHLOR)
+    if (K == 6) CH8(OR3)
+    if (K == 7) CH8(BFE)
+    if (K == 8) CH8(LSHL)
+    if (K == 9) CH8(SDWA)
+    if (K == 10) CH8(MIN3)
+    if (K == 11) CH8(MIN)
+    if (K == 12) CH8(MAD24)
+    if (K == 13) CH8(ADD3)
+    if (K == 14) CH8(XDPP)
+    if (K == 15) CH8(LSHLORDPP)
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * 32 + (threadIdx.x >> 6)] = t1 - t0;
+  if ((a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) == 0x1234567) out[100000] = 1;
+}
+
 int main() {
   uint64_t* d; hipMalloc(&d, 8 * 2048);
   const char* names[] = {"xor dep", "alignbit dep", "lshl_add_u64 dep", "add_co+addc dep (pair)",
@@ -141,6 +224,29 @@ int main() {
       hipEventElapsedTime(&ms, e0, e1); printf("rd_strip<256>  %.1f GB/s\n", n / ms / 1e6);
     }
     hipFree(buf);
+  }
+  {
+    uint8_t* src; hipMalloc(&src, 1 << 24); hipMemset(src, 3, 1 << 24);
+    for (int rep = 0; rep < 3; rep++) {
+      dma_lgkm<<<1, 64>>>(src + rep * (1 << 20), d); hipDeviceSynchronize(); hipMemcpy(h, d, 32, hipMemcpyDeviceToHost);
+      printf("ds_read+lgkm0 %llu | DMA,ds_read+lgkm0 %llu | DMA+vmcnt0 %llu (s_memtime ticks)\n",
+             (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2]);
+    }
+  }
+  {
+    uint64_t* tb; hipMalloc(&tb, 8 * 256 * 32 + 8 * 100001);
+    const char* nm[] = {"xor", "alignbit", "bitop3", "perm", "and_or", "lshl_or", "or3", "bfe", "lshlrev", "lshl_sdwa", "min3", "min", "mad_u24", "add3", "xor_dpp", "or_sdwa", "lshl_add64"};
+    void (*ks[])(uint64_t*, uint32_t) = {thr<0>, thr<1>, thr<2>, thr<3>, thr<4>, thr<5>, thr<6>, thr<7>, thr<8>, thr<9>, thr<10>, thr<11>, thr<12>, thr<13>, thr<14>, thr<15>, thr<16>};
+    for (int w : {1, 3, 4}) {
+      for (int K = 0; K < 17; K++) {
+        void (*kern)(uint64_t*, uint32_t) = ks[K];
+        kern<<<256, 256 * w>>>(tb, 1); hipDeviceSynchronize(); kern<<<256, 256 * w>>>(tb, 1); hipDeviceSynchronize();
+        static uint64_t hb[256 * 32]; hipMemcpy(hb, tb, 8 * 256 * 32, hipMemcpyDeviceToHost);
+        uint64_t mx = 0; for (int b = 0; b < 256; b++) for (int k = 0; k < 4 * w; k++) mx = hb[b * 32 + k] > mx ? hb[b * 32 + k] : mx;
+        double instr_per_simd = (double)w * 256 * 32;  // waves per SIMD x instructions per wave
+        printf("thr %-9s %d waves/SIMD: %.3f instr/cycle/SIMD (%.2f cycles per wave-instr)\n", nm[K], w, instr_per_simd / mx, mx / instr_per_simd);
+      }
+    }
   }
   lds_chase<<<1, 64>>>(d); hipDeviceSynchronize(); lds_chase<<<1, 64>>>(d); hipMemcpy(h, d, 8, hipMemcpyDeviceToHost);
   printf("ds_read_b32 chase: %.1f cycles\n", h[0] / 2000.0);
