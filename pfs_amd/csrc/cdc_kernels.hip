@@ -22,6 +22,7 @@
 // every Annotate/cut (writer.go:125-128,211), so no eligible position sees the reset window.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -590,71 +591,188 @@ PFS_DEV void msg_load_full(uint4& m0, uint4& m1, const uint8_t* p) {
 }
 
 // Last block of a segment: bytes at or past `avail` are zero (BLAKE2b pads with zeros).
-PFS_DEV void msg_load_tail(uint4& m0, uint4& m1, const uint8_t* p, int64_t avail) {
+// Two 16-byte loads and a byte mask when the 32-byte window lies inside the batch buffer
+// (bytes past the segment belong to the next segment or file); byte loads only for the
+// final block of the buffer.
+PFS_DEV uint32_t keep_bytes(int64_t k) {  // mask of the low k bytes of a dword (k may be <0, >4)
+  return k >= 4 ? 0xffffffffu : k <= 0 ? 0u : (1u << (8 * (uint32_t)k)) - 1u;
+}
+
+PFS_DEV void msg_load_tail(uint4& m0, uint4& m1, const uint8_t* p, int64_t avail,
+                           const uint8_t* end) {
+  if (p + 32 <= end) {
+    msg_load_full(m0, m1, p);
+    m0.x &= keep_bytes(avail - 0);
+    m0.y &= keep_bytes(avail - 4);
+    m0.z &= keep_bytes(avail - 8);
+    m0.w &= keep_bytes(avail - 12);
+    m1.x &= keep_bytes(avail - 16);
+    m1.y &= keep_bytes(avail - 20);
+    m1.z &= keep_bytes(avail - 24);
+    m1.w &= keep_bytes(avail - 28);
+    return;
+  }
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     uint32_t v = 0;
-    if (4 * i + 4 <= avail) {
-      __builtin_memcpy(&v, p + 4 * i, 4);
-    } else {
-      for (int b = 0; b < 4; b++)
-        if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
-    }
+    for (int b = 0; b < 4; b++)
+      if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
     w[i] = v;
   }
   m0 = make_uint4(w[0], w[1], w[2], w[3]);
   m1 = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
+// 5a. LPT order: segment indices sorted by block count, longest first (counting sort on a
+// 10-bit key, one workgroup).  The hash kernel's quads pull segments in this order, so the
+// longest serial chains start first and the short ones fill in behind them.
+PFS_DEV uint32_t lpt_key(uint64_t size) {
+  const uint64_t nblk = (size + 127) / 128;
+  const uint64_t k = nblk >> 6;  // 8 KiB granularity
+  return 1023u - (uint32_t)(k < 1023 ? k : 1023);  // ascending key = descending length
+}
+
+__global__ __launch_bounds__(kCompactBlock) void hash_order_kernel(
+    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
+    uint32_t* __restrict__ order, uint32_t* __restrict__ counter) {
+  static_assert(kCompactBlock == 1024, "one histogram bin per thread");
+  __shared__ uint32_t hist[1024];
+  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+  const uint64_t n = *seg_count;
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < n; i += kCompactBlock) atomicAdd(&hist[lpt_key(segs[i].size)], 1u);
+  __syncthreads();
+  uint64_t total;
+  const uint64_t start = block_exclusive_scan(hist[threadIdx.x], s_wave, &total);
+  hist[threadIdx.x] = (uint32_t)start;
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < n; i += kCompactBlock)
+    order[atomicAdd(&hist[lpt_key(segs[i].size)], 1u)] = (uint32_t)i;
+  if (threadIdx.x == 0) *counter = 0;
+}
+
+// 5b. BLAKE2b-256 per segment: 4 lanes (a quad) hash one segment, lane j owning column j of
+// the 4x4 state; waves stay resident and each quad pulls its next segment from the LPT
+// queue when it finishes one (one wave-aggregated atomic per refill).  The compression runs
+// with every lane enabled (a finished quad computes on stale registers and discards it), so
+// the DPP quad rotations never see a disabled lane.
+// perm(c) + d, the permutation folded into the add as a DPP source operand (v_add_co_u32_dpp
+// + v_addc_co_u32_dpp) instead of two v_mov_b32_dpp and a v_lshl_add_u64.
+template <int CTRL>
+PFS_DEV uint64_t perm_add(uint64_t c, uint64_t d) {
+  const uint32_t cl = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)c, CTRL, 0xF, 0xF, true);
+  const uint32_t ch = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(c >> 32), CTRL, 0xF, 0xF, true);
+  const uint32_t lo = cl + (uint32_t)d;
+  const uint32_t hi = ch + (uint32_t)(d >> 32) + (lo < cl ? 1u : 0u);
+  return mk64(lo, hi);
+}
+
+// G with the incoming diagonal rotation of c folded into its first use.
+#define PFS_G_PC(a, b, c, d, x, y, CC) \
+  do {                                 \
+    a = a + b + (x);                   \
+    d = xor_rotr32(d, a);              \
+    c = perm_add<CC>(c, d);            \
+    b = xor_rotr<24>(b, c);            \
+    a = a + b + (y);                   \
+    d = xor_rotr<16>(d, a);            \
+    c = c + d;                         \
+    b = xor_rotr63(b, c);              \
+  } while (0)
+
 __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
-    pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_msg[kHashBlock / 4 * 256];
-  const uint64_t quad = ((uint64_t)blockIdx.x * kHashBlock + threadIdx.x) >> 2;
-  const uint32_t j = threadIdx.x & 3u;
-  if (quad >= *seg_count) return;  // whole quads exit together
-  pfscdc_segment* seg = segs + quad;
-  const uint64_t L = seg->size;
-  const uint8_t* src = data + offs[seg->file] + seg->offset;
-  const uint32_t slot = (threadIdx.x >> 2) * 256u;  // low byte 0: perm builds the address
+    pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes) {
+  // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
+  // i&1 while the quad's next block (loaded into registers one iteration earlier) is written
+  // to the other buffer halfway through; the wave-uniform parity makes every ds_read offset
+  // an immediate (the loop body is unrolled twice).  Quad slots are kMsgStride = 160 bytes
+  // apart: at a 128- or 256-byte stride the 8 quads of a ds_read_b64 lane group (which all
+  // read the same message word) hit the same bank pair (8-way conflict, 16 LDS cycles per
+  // read); 160 bytes (40 dwords) spreads them to ~2-way on the 48 reads of a block
+  // (tools/lds_msg_layout.py).
+  constexpr uint32_t kMsgStride = 160, kMsgBuf = kHashBlock / 4 * kMsgStride;
+  __shared__ __attribute__((aligned(16))) uint8_t s_msg[2 * kMsgBuf];
+  const uint8_t* const end = data + nbytes;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t j = lane & 3u;
+  const uint64_t nseg = *seg_count;
+  const uint32_t slot = (threadIdx.x >> 2) * kMsgStride;
   uint8_t* my = s_msg + slot + 32u * j;
 
-  // LDS addresses of the 4 message words this lane consumes in each round (loop invariant)
+  // LDS addresses (buffer 0) of the 4 message words this lane consumes in each round
   uint32_t ma[12][4];
 #pragma unroll
   for (int r = 0; r < 12; r++) {
     const uint32_t pk = kSigmaPack[r][j];
 #pragma unroll
-    for (int k = 0; k < 4; k++) ma[r][k] = __builtin_amdgcn_perm(pk, slot, 0x0c0c0104u + k);
+    for (int k = 0; k < 4; k++) ma[r][k] = slot + ((pk >> (8 * k)) & 0xFFu);
   }
-
   const uint64_t iv_c = kB2IV[j];
   const uint64_t iv_d = kB2IV[4 + j];
-  uint64_t ha = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : kB2IV[j];  // digest 32, fanout/depth 1
-  uint64_t hb = kB2IV[4 + j];
+  const uint64_t h0a = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : kB2IV[j];  // digest 32, fanout/depth 1
+  const uint64_t h0b = kB2IV[4 + j];
 
-  const uint64_t nblk = L == 0 ? 1 : (L + 127) / 128;
-  uint4 m0, m1;
-  if (nblk == 1) msg_load_tail(m0, m1, src + 32 * j, (int64_t)L - 32 * (int64_t)j);
-  else msg_load_full(m0, m1, src + 32 * j);
+  bool active = false;   // this quad holds a segment
+  bool drained = false;  // wave-uniform: the queue is exhausted
+  uint64_t L = 0, nblk = 0, blk = 0;
+  const uint8_t* src = data;
+  pfscdc_segment* seg = segs;
+  uint64_t ha = 0, hb = 0;
+  uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;  // the quad's block blk+1 (lane j: bytes 32j..)
 
-  for (uint64_t blk = 0; blk < nblk; blk++) {
+  auto lds_put = [&](uint32_t buf) {
+    reinterpret_cast<uint4*>(my + buf)[0] = m0;
+    reinterpret_cast<uint4*>(my + buf)[1] = m1;
+  };
+  auto load_block = [&](uint64_t b) {  // block b of the quad's segment -> m0, m1
+    const uint8_t* p = src + b * 128 + 32 * j;
+    if (b + 1 == nblk) msg_load_tail(m0, m1, p, (int64_t)(L - b * 128) - 32 * (int64_t)j, end);
+    else msg_load_full(m0, m1, p);
+  };
+
+  auto step = [&](auto par) -> bool {
+    constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
+    if (!drained) {
+      const bool need = !active;
+      const uint64_t want = __ballot(need && j == 0);  // one bit per idle quad (its lane 0)
+      if (want) {
+        const uint32_t cnt = (uint32_t)__popcll(want);
+        const uint32_t leader = (uint32_t)__builtin_ctzll(want);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(counter, cnt);
+        base = (uint32_t)__shfl((int)base, (int)leader, 64);
+        if (need) {
+          const uint64_t below = want & ((1ULL << (lane & ~3u)) - 1);
+          const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(below);
+          if (idx < nseg) {
+            seg = segs + order[idx];
+            L = seg->size;
+            src = data + offs[seg->file] + seg->offset;
+            nblk = L == 0 ? 1 : (L + 127) / 128;
+            blk = 0;
+            ha = h0a;
+            hb = h0b;
+            active = true;
+            load_block(0);
+            lds_put(cur);
+            if (nblk > 1) load_block(1);
+          }
+        }
+        if ((uint64_t)base + cnt >= nseg) drained = true;
+      }
+    }
+    if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
+
     const bool last = blk + 1 == nblk;
-    reinterpret_cast<uint4*>(my)[0] = m0;
-    reinterpret_cast<uint4*>(my)[1] = m1;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // software pipeline: round 0's message words, then each round fetches the next one's
-    uint64_t x0 = lds_load<uint64_t>(s_msg, ma[0][0]), x1 = lds_load<uint64_t>(s_msg, ma[0][1]);
-    uint64_t x2 = lds_load<uint64_t>(s_msg, ma[0][2]), x3 = lds_load<uint64_t>(s_msg, ma[0][3]);
-    if (!last) {  // prefetch the next block into registers while this one compresses
-      const uint64_t nb = blk + 1;
-      const uint8_t* p = src + nb * 128 + 32 * j;
-      if (nb + 1 == nblk) msg_load_tail(m0, m1, p, (int64_t)(L - nb * 128) - 32 * (int64_t)j);
-      else msg_load_full(m0, m1, p);
-    }
+    uint64_t x0 = lds_load<uint64_t>(s_msg + cur, ma[0][0]), x1 = lds_load<uint64_t>(s_msg + cur, ma[0][1]);
+    uint64_t x2 = lds_load<uint64_t>(s_msg + cur, ma[0][2]), x3 = lds_load<uint64_t>(s_msg + cur, ma[0][3]);
     const uint64_t t = last ? L : (blk + 1) * 128;
     uint64_t a = ha, b = hb, c = iv_c;
     uint64_t d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
@@ -662,10 +780,10 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     for (int r = 0; r < 12; r++) {
       uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
       if (r < 11) {
-        y0 = lds_load<uint64_t>(s_msg, ma[r + 1][0]);
-        y1 = lds_load<uint64_t>(s_msg, ma[r + 1][1]);
-        y2 = lds_load<uint64_t>(s_msg, ma[r + 1][2]);
-        y3 = lds_load<uint64_t>(s_msg, ma[r + 1][3]);
+        y0 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][0]);
+        y1 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][1]);
+        y2 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][2]);
+        y3 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][3]);
       }
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
       c = quad_perm64<0x4E>(c);            // c <- v[8+(j+2)%4]
@@ -676,12 +794,181 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
       d = quad_perm64<0x39>(d);
       b = quad_perm64<0x93>(b);
       x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+      if (r == 5 && active && !last) {  // block blk+1 -> the other buffer; fetch blk+2
+        lds_put(nxt);
+        if (blk + 2 < nblk) load_block(blk + 2);
+      }
     }
     ha ^= a ^ c;
     hb ^= b ^ d;
+    if (active) {
+      blk++;
+      if (last) {  // digest = h[0..3] little endian; lane j owns h[j]
+        reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
+        active = false;
+      }
+    }
+    return true;
+  };
+  while (step(std::integral_constant<uint32_t, 0>{}) && step(std::integral_constant<uint32_t, 1>{})) {
   }
-  // digest = h[0..3] little endian; lane j owns h[j]
-  reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
+}
+
+// 5c. BLAKE2b-256, one lane per segment.  No cross-lane traffic at all: the 16-word state,
+// the chaining value and the message block live in the lane's registers, and the sigma
+// schedule is resolved at compile time (every round fully unrolled), so a block costs the
+// bare 96 G functions (6 v_lshl_add_u64 + 8 v_xor_b32 + 6 v_alignbit_b32 each) and its
+// loads.  The 4-lane kernel above spends ~30% more VALU per block on DPP quad rotations
+// and LDS message gathers; on gfx950 nearly every VALU op holds the SIMD-32 for 4 cycles
+// (v_xor_b32 for 2), so instructions per chain-block, not latency, set the throughput once
+// enough segments are in flight.  Lanes pull segments from the same LPT queue.
+constexpr uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+};
+constexpr uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                             0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                             0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+// One 128-byte block for this lane: eight 16-byte loads.
+PFS_DEV void blk_load_full(uint4 (&m)[8], const uint8_t* p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) __builtin_memcpy(&m[i], p + 16 * i, 16);
+}
+
+// Last block of a segment: bytes at or past `avail` zeroed (see msg_load_tail).
+PFS_DEV void blk_load_tail(uint4 (&m)[8], const uint8_t* p, int64_t avail, const uint8_t* end) {
+  if (p + 128 <= end) {
+    blk_load_full(m, p);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      m[i].x &= keep_bytes(avail - 16 * i - 0);
+      m[i].y &= keep_bytes(avail - 16 * i - 4);
+      m[i].z &= keep_bytes(avail - 16 * i - 8);
+      m[i].w &= keep_bytes(avail - 16 * i - 12);
+    }
+    return;
+  }
+  uint32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint32_t v = 0;
+    for (int b = 0; b < 4; b++)
+      if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
+    w[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Block `b` (0-based) of a segment of L bytes into m.
+PFS_DEV void blk_load(uint4 (&m)[8], const uint8_t* src, uint64_t b, uint64_t L, uint64_t nblk,
+                      const uint8_t* end) {
+  const uint8_t* p = src + b * 128;
+  if (b + 1 == nblk) blk_load_tail(m, p, (int64_t)(L - b * 128), end);
+  else blk_load_full(m, p);
+}
+
+__global__ __launch_bounds__(kHashLaneBlock) void blake2b_lane_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nseg = *seg_count;
+  const uint8_t* const end = data + nbytes;
+  bool active = false;   // this lane holds a segment
+  bool drained = false;  // wave-uniform: the queue is exhausted
+  uint64_t L = 0, nblk = 0, blk = 0;
+  const uint8_t* src = data;
+  pfscdc_segment* seg = segs;
+  uint64_t h[8];
+  uint4 m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    h[i] = 0;
+    m[i] = make_uint4(0, 0, 0, 0);
+  }
+
+  while (true) {
+    if (!drained) {
+      const bool need = !active;
+      const uint64_t want = __ballot(need);
+      if (want) {
+        const uint32_t cnt = (uint32_t)__popcll(want);
+        const uint32_t leader = (uint32_t)__builtin_ctzll(want);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(counter, cnt);
+        base = (uint32_t)__shfl((int)base, (int)leader, 64);
+        if (need) {
+          const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(want & ((1ULL << lane) - 1));
+          if (idx < nseg) {
+            seg = segs + order[idx];
+            L = seg->size;
+            src = data + offs[seg->file] + seg->offset;
+            nblk = L == 0 ? 1 : (L + 127) / 128;
+            blk = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) h[i] = kIV[i];
+            h[0] ^= 0x01010020ULL;  // digest 32 bytes, fanout 1, depth 1
+            active = true;
+            blk_load(m, src, 0, L, nblk, end);
+          }
+        }
+        if ((uint64_t)base + cnt >= nseg) drained = true;
+      }
+    }
+    if (__ballot(active) == 0) break;  // every lane idle and the queue empty
+
+    const bool last = blk + 1 == nblk;
+    uint64_t x[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      x[2 * i] = mk64(m[i].x, m[i].y);
+      x[2 * i + 1] = mk64(m[i].z, m[i].w);
+    }
+    if (active && !last) blk_load(m, src, blk + 1, L, nblk, end);  // prefetch the next block
+    const uint64_t t = last ? L : (blk + 1) * 128;
+    uint64_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      v[i] = h[i];
+      v[8 + i] = kIV[i];
+    }
+    v[12] ^= t;
+    v[14] ^= last ? ~0ULL : 0ULL;
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+      PFS_G(v[0], v[4], v[8], v[12], x[kSigma[r][0]], x[kSigma[r][1]]);
+      PFS_G(v[1], v[5], v[9], v[13], x[kSigma[r][2]], x[kSigma[r][3]]);
+      PFS_G(v[2], v[6], v[10], v[14], x[kSigma[r][4]], x[kSigma[r][5]]);
+      PFS_G(v[3], v[7], v[11], v[15], x[kSigma[r][6]], x[kSigma[r][7]]);
+      PFS_G(v[0], v[5], v[10], v[15], x[kSigma[r][8]], x[kSigma[r][9]]);
+      PFS_G(v[1], v[6], v[11], v[12], x[kSigma[r][10]], x[kSigma[r][11]]);
+      PFS_G(v[2], v[7], v[8], v[13], x[kSigma[r][12]], x[kSigma[r][13]]);
+      PFS_G(v[3], v[4], v[9], v[14], x[kSigma[r][14]], x[kSigma[r][15]]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
+    if (active) {
+      blk++;
+      if (last) {  // digest = h[0..3] little endian
+        uint4* out = reinterpret_cast<uint4*>(seg->hash);
+        out[0] = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
+        out[1] = make_uint4((uint32_t)h[2], (uint32_t)(h[2] >> 32), (uint32_t)h[3], (uint32_t)(h[3] >> 32));
+        active = false;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -785,11 +1072,30 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 }
 
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
-                          const uint64_t* seg_count, uint64_t max_segments, hipStream_t st) {
+                          const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
+                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st) {
   if (max_segments == 0) return hipSuccess;
+  hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
+  // resident waves: kHashWavesPerSimd per SIMD (4 SIMDs per CU), no more than the segments need
+  static const int waves_per_simd = [] {  // tuning knob (PFSCDC_HASH_WAVES), default 2
+    const char* e = getenv("PFSCDC_HASH_WAVES");
+    const int w = e ? atoi(e) : kHashWavesPerSimd;
+    return w >= 1 && w <= 8 ? w : kHashWavesPerSimd;
+  }();
+  if (kHashLanesPerSegment == 1) {
+    const uint64_t need = (max_segments + kHashLaneBlock - 1) / kHashLaneBlock;
+    const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashLaneBlock / 64);
+    const uint64_t grid = need < full ? need : full;
+    blake2b_lane_kernel<<<(unsigned)grid, kHashLaneBlock, 0, st>>>(data, offs, segs, seg_count,
+                                                                   order, counter, nbytes);
+    return hipGetLastError();
+  }
   const uint64_t quads_per_block = kHashBlock / 4;
-  const uint64_t grid = (max_segments + quads_per_block - 1) / quads_per_block;
-  blake2b_kernel<<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count);
+  const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
+  const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
+  const uint64_t grid = need < full ? need : full;
+  blake2b_kernel<<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order, counter,
+                                                     nbytes);
   return hipGetLastError();
 }
 

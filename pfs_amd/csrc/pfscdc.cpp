@@ -77,6 +77,7 @@ struct pfscdc_ctx {
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
+  DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
   PinnedBuf<pfscdc_segment> h_segs;
   hipEvent_t ev[6] = {};
@@ -210,6 +211,8 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_seg_begin.release();
   c->d_slots.release();
   c->d_segs.release();
+  c->d_order.release();
+  c->d_qctr.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -269,6 +272,8 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, c->d_seg_begin.ensure(nfiles + 1));
   HIP_OK(c, c->d_slots.ensure(cap));
   HIP_OK(c, c->d_segs.ensure(cap));
+  HIP_OK(c, c->d_order.ensure(cap));
+  HIP_OK(c, c->d_qctr.ensure(1));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
@@ -314,7 +319,8 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   }
   HIP_OK(c, hipEventRecord(c->ev[3], st));
   if (nfiles)
-    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap, st));
+    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
+                             c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)

@@ -20,7 +20,16 @@ constexpr uint32_t kScanLdsBytes = kScanCandLds + 16 + 4 * kTileCandCap;
 static_assert(kScanLdsBytes <= 160 * 1024, "scan kernel LDS budget");
 constexpr int kCompactBlock = 1024;
 constexpr int kSelectBlock = 256;   // 4 files (waves) per block
-constexpr int kHashBlock = 256;     // 64 segments per block
+constexpr int kHashBlock = 256;     // 64 quads (one segment each at a time) per block
+#ifndef PFS_HASH_WAVES_PER_SIMD
+#define PFS_HASH_WAVES_PER_SIMD 2
+#endif
+constexpr int kHashWavesPerSimd = PFS_HASH_WAVES_PER_SIMD;  // 2 saturate VALU issue (SIMD-32)
+#ifndef PFS_HASH_LANES
+#define PFS_HASH_LANES 4
+#endif
+constexpr int kHashLanesPerSegment = PFS_HASH_LANES;  // 1: blake2b_lane_kernel, 4: blake2b_kernel
+constexpr int kHashLaneBlock = 256;
 constexpr uint64_t kDenseBit = 1ULL << 63;
 constexpr uint64_t kNone = ~0ULL;
 constexpr uint64_t kTailBytes = 256;  // zero-padded copy of the final partial 64-byte block
@@ -50,7 +59,8 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
                              const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
                              uint64_t* seg_begin, hipStream_t st);
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
-                          const uint64_t* seg_count, uint64_t max_segments, hipStream_t st);
+                          const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
+                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st);
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
                         hipStream_t st);
 

@@ -168,6 +168,9 @@ template <int K> __global__ void thr(uint64_t* out, uint32_t seed) {
 #define MAD24(R) "v_mad_u32_u24 " R ", " R ", %8, %9\n"
 #define ADD3(R) "v_add3_u32 " R ", " R ", %8, %9\n"
 #define XDPP(R) "v_xor_b32_dpp " R ", %8, " R " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+#define MDPP(R) "v_mov_b32_dpp " R ", %8 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+#define ADDC(R) "v_add_co_u32 " R ", vcc, " R ", %8\nv_addc_co_u32 %9, vcc, %9, %8, vcc\n"
+#define ADDDPP(R) "v_add_co_u32_dpp " R ", vcc, %8, " R " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
 #define LSHLORDPP(R) "v_or_b32_sdwa " R ", %8, " R " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD\n"
     if (K == 0) CH8(XOR)
     if (K == 1) CH8(ALB)
@@ -185,6 +188,11 @@ template <int K> __global__ void thr(uint64_t* out, uint32_t seed) {
     if (K == 13) CH8(ADD3)
     if (K == 14) CH8(XDPP)
     if (K == 15) CH8(LSHLORDPP)
+    if (K == 17) CH8(MDPP)
+    if (K == 18) asm volatile(".rept 4\n" ADDC("%0") ADDC("%1") ADDC("%2") ADDC("%3") ADDC("%4") ADDC("%5") ADDC("%6") ADDC("%7") ".endr\n"
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "v"(c) : "vcc");
+    if (K == 19) asm volatile(".rept 4\n" ADDDPP("%0") ADDDPP("%1") ADDDPP("%2") ADDDPP("%3") ADDDPP("%4") ADDDPP("%5") ADDDPP("%6") ADDDPP("%7") ".endr\n"
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "v"(c) : "vcc");
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) out[blockIdx.x * 32 + (threadIdx.x >> 6)] = t1 - t0;
@@ -235,10 +243,10 @@ int main() {
   }
   {
     uint64_t* tb; hipMalloc(&tb, 8 * 256 * 32 + 8 * 100001);
-    const char* nm[] = {"xor", "alignbit", "bitop3", "perm", "and_or", "lshl_or", "or3", "bfe", "lshlrev", "lshl_sdwa", "min3", "min", "mad_u24", "add3", "xor_dpp", "or_sdwa", "lshl_add64"};
-    void (*ks[])(uint64_t*, uint32_t) = {thr<0>, thr<1>, thr<2>, thr<3>, thr<4>, thr<5>, thr<6>, thr<7>, thr<8>, thr<9>, thr<10>, thr<11>, thr<12>, thr<13>, thr<14>, thr<15>, thr<16>};
-    for (int w : {1, 3, 4}) {
-      for (int K = 0; K < 17; K++) {
+    const char* nm[] = {"xor", "alignbit", "bitop3", "perm", "and_or", "lshl_or", "or3", "bfe", "lshlrev", "lshl_sdwa", "min3", "min", "mad_u24", "add3", "xor_dpp", "or_sdwa", "lshl_add64", "mov_dpp", "addco+addc", "addco_dpp"};
+    void (*ks[])(uint64_t*, uint32_t) = {thr<0>, thr<1>, thr<2>, thr<3>, thr<4>, thr<5>, thr<6>, thr<7>, thr<8>, thr<9>, thr<10>, thr<11>, thr<12>, thr<13>, thr<14>, thr<15>, thr<16>, thr<17>, thr<18>, thr<19>};
+    for (int w : {1, 2, 4}) {
+      for (int K = 0; K < 20; K++) {
         void (*kern)(uint64_t*, uint32_t) = ks[K];
         kern<<<256, 256 * w>>>(tb, 1); hipDeviceSynchronize(); kern<<<256, 256 * w>>>(tb, 1); hipDeviceSynchronize();
         static uint64_t hb[256 * 32]; hipMemcpy(hb, tb, 8 * 256 * 32, hipMemcpyDeviceToHost);
