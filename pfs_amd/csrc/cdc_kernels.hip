@@ -16,8 +16,11 @@
 //   3. select_kernel       one wave per file: serial cut selection over the sparse list
 //                          (writer.go:168,179 min/max rule), dense tiles re-rolled in-wave.
 //   4. segcompact_kernel   one workgroup: per-file segment counts -> dense segment list.
-//   5. blake2b_kernel      4 lanes per segment (one BLAKE2b column each, DPP quad
-//                          rotations for the diagonal step), message via LDS.
+//   5. hash_order_kernel   one workgroup: segments sorted longest-first (LPT queue order).
+//      blake2b_kernel      resident waves, 4 lanes (a quad) per segment, one BLAKE2b column
+//                          each (DPP quad rotations for the diagonal step), message words
+//                          through double-buffered LDS; quads pull the next segment from
+//                          the queue when one finishes.  VALU-issue bound.
 // Why the hash of a cut only needs the last 64 bytes: min >= 64 and hash+seglen reset at
 // every Annotate/cut (writer.go:125-128,211), so no eligible position sees the reset window.
 #include <hip/hip_runtime.h>

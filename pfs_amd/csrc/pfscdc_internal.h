@@ -28,7 +28,7 @@ constexpr int kHashWavesPerSimd = PFS_HASH_WAVES_PER_SIMD;  // 2 saturate VALU i
 #ifndef PFS_HASH_LANES
 #define PFS_HASH_LANES 4
 #endif
-constexpr int kHashLanesPerSegment = PFS_HASH_LANES;  // 1: blake2b_lane_kernel, 4: blake2b_kernel
+constexpr int kHashLanesPerSegment = PFS_HASH_LANES;  // 4: blake2b_kernel (product), 1: blake2b_lane_kernel (A/B)
 constexpr int kHashLaneBlock = 256;
 constexpr uint64_t kDenseBit = 1ULL << 63;
 constexpr uint64_t kNone = ~0ULL;
