@@ -2,19 +2,28 @@
 """Benchmark of the MI355X PFS chunk-ingest path (BASELINE.json metric).
 
 Metric: GiB/s of file bytes through CDC rolling hash + per-segment BLAKE2b-256 content hash
-with inputs already resident in HBM.  Workload at N=1 = BASELINE.json configs[1]: 1024
-independent 4 MiB buffers (one file = one chunk stream each), synthetic bytes (seeded
-splitmix64 stream, see include/pfscdc.h).  A "step" = one pass of the whole path over the
-batch: candidate scan -> compaction -> cut selection -> BLAKE2b of every segment -> segment
-records back on the host (and, for N>1, the RCCL all-gather of the chunk-ref index).
+with inputs already resident in HBM.  A "step" = one pass of the whole path over the step's
+files: candidate scan -> compaction -> cut selection -> LPT order -> BLAKE2b of every
+segment -> segment records back on the host (and, for N>1 or --config c5, the gather of the
+chunk-ref index: RCCL all-gather for N>1).
 
-N>1 (torch.distributed.run, one rank per GPU): every rank owns its own 1024 x 4 MiB shard
-of a commit (weak scaling); value = all ranks' bytes / max-over-ranks time.
+Workloads (--config, BASELINE.json configs[i]; all synthetic, generated in HBM):
+  c2 (default, the headline): configs[1], batches of 1024 independent 4 MiB buffers.  One
+     step = --group such batches (default 32 = 128 GiB resident), because BLAKE2b chains are
+     serial and the hash needs ~16K+ segments in flight to fill the GPU.
+     N>1: every rank its own 32-batch shard (weak scaling).
+  c3: configs[2], one 10 GiB stream per GPU (block-parallel scan with halos; the serial cut
+     set is checked against the CPU oracle on the whole stream).
+  c4: configs[3], a 100 GiB commit of 10,000 files (10,737,418 B each, +2,400 on the last),
+     sharded by file across ranks (strong scaling), RCCL all-gather of the chunk-ref index.
+  c5: configs[4], the c4 layout with dedup-heavy bytes: 1 MiB blocks, half of them copies of
+     64 pooled blocks (--dedup blocks) or half of the files copies of 64 pooled files
+     (--dedup files); reports the segment / byte dedup hit rate of the gathered index.
 
-Extra objects on the JSON line: ``roofline`` (dominant kernel, HIP events on the
-library's stream), ``roofline_cdc`` (the scan kernel), ``cpu_baseline`` (C restatement of
-the reference chunker on the host cores, rank 0 at N=1), ``e2e`` (pinned host input incl.
-PCIe H2D), ``parity`` (GPU records == CPU records on the measured workload).
+Extra objects on the JSON line: ``roofline`` (dominant kernel, HIP events on the library's
+stream), ``roofline_cdc`` (the scan kernel), ``cpu_baseline`` (C restatement of the
+reference chunker on the host cores, rank 0 at N=1), ``e2e`` (pinned host input incl. PCIe
+H2D, c2 only), ``parity`` (GPU records == CPU oracle records on a sample of the workload).
 """
 import argparse
 import json
@@ -27,6 +36,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
+C4_FILES, C4_FILE_BYTES, C4_TAIL = 10_000, 10_737_418, 2_400
+C3_BYTES = 10 * (1 << 30)
 
 
 def parse():
@@ -34,13 +45,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--files", type=int, default=1024)
-    ap.add_argument("--file-bytes", type=int, default=4 << 20)
-    ap.add_argument("--seed", type=int, default=0xC2)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--files", type=int, default=1024, help="c2: files per configs[1] batch")
+    ap.add_argument("--file-bytes", type=int, default=4 << 20, help="c2: bytes per file")
     ap.add_argument("--group", type=int, default=32,
-                    help="configs[1] batches per step (one launch group, resident in HBM "
-                         "together): BLAKE2b chains are serial, so the hash needs ~32K "
-                         "segments in flight to fill 1024 SIMDs")
+                    help="c2: configs[1] batches per step (one launch group, resident in HBM "
+                         "together)")
+    ap.add_argument("--dedup", default="blocks", choices=["blocks", "files"], help="c5 layout")
+    ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="steps in flight (one GPU context + input buffer each)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
@@ -48,6 +60,76 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--traffic-json", default="", help="per-launch HBM bytes from a PMC run")
     return ap.parse_args()
+
+
+def workload(args, world, rank):
+    """This rank's files for one step: (sizes, global id of its first file, seed, synth
+    mode, config info, scaling)."""
+    from pfs_amd import distributed as pd
+    from pfs_amd.cdc import SYNTH_DEDUP_BLOCKS, SYNTH_DEDUP_FILES, SYNTH_RANDOM
+
+    if args.config == "c2":
+        G = max(1, args.group)
+        n = args.files * G
+        seed = 0xC2 if args.seed < 0 else args.seed
+        info = {"workload": "configs[1]: batches of %d x %d B independent buffers; %d batches "
+                            "per step (one launch group) per GPU" % (args.files, args.file_bytes, G),
+                "files_per_step": n, "file_bytes": args.file_bytes, "batches_per_step": G}
+        return [args.file_bytes] * n, 0, seed + 1000 * rank, SYNTH_RANDOM, info, "weak"
+    if args.config == "c3":
+        seed = 0xC3 if args.seed < 0 else args.seed
+        info = {"workload": "configs[2]: one %d B stream per GPU" % C3_BYTES,
+                "files_per_step": 1, "file_bytes": C3_BYTES}
+        return [C3_BYTES], 0, seed + 1000 * rank, SYNTH_RANDOM, info, "weak"
+    sizes = [C4_FILE_BYTES] * C4_FILES
+    sizes[-1] += C4_TAIL
+    b, e = pd.shard_files(sizes, world)[rank]
+    mode = SYNTH_RANDOM
+    if args.config == "c5":
+        mode = SYNTH_DEDUP_BLOCKS if args.dedup == "blocks" else SYNTH_DEDUP_FILES
+    seed = (0xC4 if args.config == "c4" else 0xC5) if args.seed < 0 else args.seed
+    what = "100 GiB" if args.config == "c4" else "100 GiB dedup-heavy (%s)" % args.dedup
+    info = {"workload": "configs[%d]: %s commit of %d files (%d B each, +%d on the last), "
+                        "sharded by file over %d GPU(s)"
+                        % (3 if args.config == "c4" else 4, what, C4_FILES, C4_FILE_BYTES,
+                           C4_TAIL, world),
+            "files_per_step": e - b, "files_total": C4_FILES}
+    if args.config == "c5":
+        info["dedup"] = ("1 MiB blocks, p=1/2 a copy of one of 64 pooled blocks"
+                         if args.dedup == "blocks" else
+                         "whole files, p=1/2 a copy of one of 64 pooled files")
+    return sizes[b:e], b, seed, mode, info, "strong"
+
+
+def fill(chunker, tensor, sizes, fbase, seed, mode, np):
+    """Generate this rank's files; file f of the shard is file fbase + f of the commit (the
+    generator keys bytes by file index, so empty files are put in front of the shard)."""
+    offs = np.zeros(fbase + len(sizes) + 1, dtype=np.uint64)
+    offs[fbase + 1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
+    chunker.fill_synthetic(tensor, offs, seed, mode)
+
+
+def local_index(segments, fbase):
+    out = segments.copy()
+    out["file"] = out["file"] + fbase
+    return out
+
+
+def hit_rate(index):
+    """Fraction of segments (and bytes) whose BLAKE2b digest appeared earlier in commit
+    order: the chunk-level dedup a content-addressed store gets from these DataRefs."""
+    seen = set()
+    hit_s = hit_b = 0
+    for h, size in zip(index["hash"], index["size"]):
+        key = h.tobytes()
+        if key in seen:
+            hit_s += 1
+            hit_b += int(size)
+        else:
+            seen.add(key)
+    nb = int(index["size"].sum()) if len(index) else 0
+    return {"segments": int(len(index)), "segment_hit_rate": round(hit_s / max(len(index), 1), 5),
+            "byte_hit_rate": round(hit_b / max(nb, 1), 5), "unique_digests": len(seen)}
 
 
 def main():
@@ -70,21 +152,31 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     params = ChunkParams()  # reference defaults: avgBits 23, seed 1, min 1 MB, max 20 MB
-    G = max(1, args.group)
-    bfiles, fbytes = args.files, args.file_bytes  # one configs[1] batch
-    nfiles = bfiles * G                             # files per step
-    offs = np.arange(nfiles + 1, dtype=np.uint64) * np.uint64(fbytes)
+    sizes, fbase, seed, mode, info, scaling = workload(args, world, rank)
+    nfiles = len(sizes)
+    offs = np.zeros(nfiles + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
     total = int(offs[-1])
-    bbytes = bfiles * fbytes
+    # parity / CPU-baseline sample: the first configs[1] batch (c2), the whole stream (c3),
+    # or the shard's first ~4 GiB of files (c4/c5)
+    if args.config == "c2":
+        sfiles = min(args.files, nfiles)
+    elif args.config == "c3":
+        sfiles = 1
+    else:
+        sfiles = min(nfiles, max(1, int((4 << 30) // max(sizes[0], 1))))
+    sbytes = int(offs[sfiles])
+
     S = max(1, args.inflight)
     chunkers = [Chunker(params, device=local) for _ in range(S)]
     batches = []
-    for k in range(S):  # rank r's shard of the commit; batch k = its k-th 1024-file batch
+    for k in range(S):
         t = torch.empty(total, dtype=torch.uint8, device=dev)
-        chunkers[k].fill_synthetic(t, offs, args.seed + 1000 * rank + k)
+        fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
         batches.append(t)
     chunker, data = chunkers[0], batches[0]
-    cap = pd.max_segments([fbytes] * nfiles, params.min_chunk)
+    cap = pd.max_segments(sizes, params.min_chunk)
+    gather = world > 1 or args.config == "c5"
     torch.cuda.synchronize()
     acc = {"scan": 0.0, "compact": 0.0, "select": 0.0, "hash": 0.0, "total": 0.0}
     pending = [False] * S
@@ -93,8 +185,9 @@ def main():
     def finish(k, record):
         res = chunkers[k].wait()
         pending[k] = False
-        if world > 1:
-            pd.gather_index(res.segments, rank * nfiles, cap, device=dev)
+        if gather:
+            last["index"] = pd.gather_index(res.segments, fbase, cap, device=dev) \
+                if world > 1 else local_index(res.segments, fbase)
         if record:
             for name, v in chunkers[k].timings().items():
                 acc[name] += v
@@ -124,15 +217,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    bytes_step = total
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        bytes_step = int(bt.item())
 
     K = max(args.steps, 1)
     avg = {k: v / K for k, v in acc.items()}
-    bytes_all = float(total) * world * args.steps
-    value = bytes_all / elapsed / GIB
+    value = float(bytes_step) * args.steps / elapsed / GIB
     ms_per_step = elapsed * 1e3 / K
 
     def roof(ms):
@@ -151,36 +247,36 @@ def main():
         roofline["traffic"] = tj.get(roofline["kernel"])
         roofline_cdc["traffic"] = tj.get("cdc_scan_kernel")
 
+    info.update({"steps_in_flight": S,
+                 "params": {"average_bits": params.average_bits, "seed": params.seed,
+                            "min": params.min_chunk, "max": params.max_chunk},
+                 "parallelism": "file-sharded x%d, RCCL all-gather of chunk-ref index" % world
+                 if world > 1 else "single GPU"})
     out = {
         "metric": "GiB/s device-resident CDC rolling-hash + chunk content-hash",
         "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)",
-        "config": {"workload": "configs[1]: batches of %d x %d B independent buffers; %d batches "
-                               "per step (one launch group) per GPU" % (bfiles, fbytes, G),
-                   "files_per_step": nfiles, "file_bytes": fbytes, "batches_per_step": G,
-                   "steps_in_flight": S,
-                   "params": {"average_bits": params.average_bits, "seed": params.seed,
-                              "min": params.min_chunk, "max": params.max_chunk},
-                   "parallelism": "file-sharded x%d, RCCL all-gather of chunk-ref index" % world
-                   if world > 1 else "single GPU"},
+        "config": info,
         "segments_per_step": int(len(res.segments)),
         "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
-        "note": "kernel_ms / roofline durations are per step (HIP events on each context's "
-                "stream); with steps_in_flight > 1 steps overlap on the GPU",
+        "note": "kernel_ms / roofline durations are per step on this rank (HIP events on the "
+                "library's stream); the hash is VALU-issue bound, not HBM bound (DESIGN.md §4)",
         "cdc_only_gib_s": round(total / (avg["scan"] * 1e-3) / GIB, 2) if avg["scan"] else None,
         "roofline": roofline,
         "roofline_cdc": roofline_cdc,
     }
 
-    if rank == 0 and world == 1 and not args.no_e2e:
-        # PCIe-inclusive: pinned host batch -> H2D -> path -> records back (not `value`)
-        # one configs[1] batch (4 GiB) per call, G calls: the host side streams batches
-        host = torch.empty(bbytes, dtype=torch.uint8, pin_memory=True)
-        host.copy_(data[:bbytes])
+    if gather and rank == 0 and "index" in last:
+        out["dedup"] = hit_rate(last["index"])
+
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e:
+        # one configs[1] batch (4 GiB) per call from pinned host memory
+        host = torch.empty(sbytes, dtype=torch.uint8, pin_memory=True)
+        host.copy_(data[:sbytes])
         hnp = host.numpy()
-        boffs = offs[:bfiles + 1]
+        boffs = offs[:sfiles + 1]
         e2e_chunker = Chunker(params, device=local)
         e2e_chunker.scan(hnp, boffs)
         torch.cuda.synchronize()
@@ -189,7 +285,7 @@ def main():
         for _ in range(n_e2e):
             e2e_chunker.scan(hnp, boffs)
         te = (time.perf_counter() - t0) / n_e2e
-        out["e2e"] = {"value": round(bbytes / te / GIB, 3), "unit": "GiB/s",
+        out["e2e"] = {"value": round(sbytes / te / GIB, 3), "unit": "GiB/s",
                       "ms_per_batch": round(te * 1e3, 3),
                       "note": "one configs[1] batch from pinned host memory: hipMemcpyAsync "
                               "H2D + kernels + records D2H, serial (no overlap)"}
@@ -201,17 +297,22 @@ def main():
         from oracle import coracle
 
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        hdata = data[:bbytes].cpu().numpy()  # the step's first configs[1] batch
+        hdata = data[:sbytes].cpu().numpy()
         p = och.Params(params.average_bits, params.seed, params.min_chunk, params.max_chunk)
-        boffs = offs[:bfiles + 1]
-        coracle.segment_files(hdata[:fbytes], offs[:2], p, nthreads=1)  # load/warm
+        soffs = offs[:sfiles + 1]
+        warm = min(sbytes, 1 << 20)
+        coracle.segment_files(hdata[:warm], [0, warm], p)  # load + warm
         t0 = time.perf_counter()
-        segs, begin = coracle.segment_files(hdata, boffs, p, nthreads=threads)
+        segs, begin = coracle.segment_files(hdata, soffs, p, nthreads=threads)
         tc = time.perf_counter() - t0
-        ns1 = max(1, min(bfiles, 32))
-        t0 = time.perf_counter()
-        coracle.segment_files(hdata[:ns1 * fbytes], offs[:ns1 + 1], p, nthreads=1)
-        t1c = time.perf_counter() - t0
+        used = min(threads, sfiles)
+        ns1 = max(1, min(sfiles, 32))
+        if sfiles > 1:
+            t0 = time.perf_counter()
+            coracle.segment_files(hdata[:int(offs[ns1])], offs[:ns1 + 1], p, nthreads=1)
+            t1 = int(offs[ns1]) / (time.perf_counter() - t0) / GIB
+        else:
+            t1 = sbytes / tc / GIB
         import platform
         cpu_model = platform.processor() or ""
         try:
@@ -221,18 +322,25 @@ def main():
                     break
         except OSError:
             pass
+        what = {"c2": "the step's first configs[1] batch", "c3": "the whole stream"}.get(
+            args.config, "the shard's first files")
         out["cpu_baseline"] = {
-            "value": round(bbytes / tc / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "value": round(sbytes / tc / GIB, 3), "unit": "GiB/s", "cores": used,
             "kind": "port",
-            "sample": "one configs[1] batch (%d x %d B, the step's first) on %d threads; "
-                      "single-thread rate from %d files" % (bfiles, fbytes, threads, ns1),
-            "single_thread_gib_s": round(ns1 * fbytes / t1c / GIB, 4),
+            "sample": "%d file(s), %d B (%s) on %d thread(s), files spread over threads; "
+                      "single-thread rate from %d file(s)" % (sfiles, sbytes, what, used, ns1),
+            "single_thread_gib_s": round(t1, 4),
             "cpu_model": cpu_model}
-        g = res.segments[:int(res.file_begin[bfiles])]
+        g = res.segments[:int(res.file_begin[sfiles])]
         same = len(g) == len(segs) and all(np.array_equal(g[f], segs[f]) for f in
                                            ("offset", "size", "file", "flags", "hash"))
         out["parity"] = {"gpu_equals_cpu_oracle": bool(same), "segments": int(len(segs)),
-                         "checked": "first configs[1] batch of the last measured step"}
+                         "checked": "the cpu_baseline sample, last measured step"}
+        if args.config == "c5" and "index" in last:
+            # the oracle's digests of the sample give the same hit rate as the GPU's
+            ref = local_index(segs, fbase)
+            out["parity"]["sample_hit_rate_gpu"] = hit_rate(last["index"][:len(ref)])
+            out["parity"]["sample_hit_rate_oracle"] = hit_rate(ref)
 
     if rank == 0:
         print(json.dumps(out))

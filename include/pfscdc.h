@@ -112,6 +112,18 @@ void pfscdc_host_free(void* p);
 int pfscdc_fill_synthetic(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* file_offsets,
                           uint32_t nfiles, uint64_t seed);
 
+/* Dedup-heavy variants (BASELINE configs[4]).  With m(x) the murmur3 64-bit finalizer:
+ *  PFSCDC_SYNTH_DEDUP_BLOCKS: the 1 MiB block k of file f is, when
+ *    h = m((seed << 48) ^ (f << 24) ^ k ^ 0xC5C5C5C5) is odd, a copy of pooled block
+ *    (h >> 1) & 63, whose word w is splitmix64-finalize(((2^23 + id) << 40 | w) + gamma);
+ *  PFSCDC_SYNTH_DEDUP_FILES: the same decision per whole file with
+ *    h = m((seed << 48) ^ (f << 24) ^ 0x5EEDF11E), the pooled file's words indexed from 0. */
+#define PFSCDC_SYNTH_RANDOM 0u
+#define PFSCDC_SYNTH_DEDUP_BLOCKS 1u
+#define PFSCDC_SYNTH_DEDUP_FILES 2u
+int pfscdc_fill_synthetic_ex(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* file_offsets,
+                             uint32_t nfiles, uint64_t seed, uint32_t mode);
+
 /* ---- chunk.Writer mirror (writer.go:52-438) ------------------------------------------
  * A writer buffers annotated bytes in host memory, runs them through pfscdc_scan in
  * batches of whole files, assembles chunks exactly as createChunk/Annotate do (including

@@ -30,7 +30,7 @@ EXPORTED = [
     "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
-    "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_writer_create",
+    "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
     "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
 ]
@@ -128,6 +128,7 @@ def load() -> C.CDLL:
             "pfscdc_host_alloc": (vp, [u64]),
             "pfscdc_host_free": (None, [vp]),
             "pfscdc_fill_synthetic": (i32, [vp, vp, P(u64), u32, u64]),
+            "pfscdc_fill_synthetic_ex": (i32, [vp, vp, P(u64), u32, u64, u32]),
             "pfscdc_writer_create": (i32, [vp, WRITER_CB, vp, u64, P(vp)]),
             "pfscdc_writer_annotate": (i32, [vp, u64]),
             "pfscdc_writer_write": (i32, [vp, vp, u64]),

@@ -16,6 +16,9 @@ import numpy as np
 from . import _lib
 
 
+SYNTH_RANDOM, SYNTH_DEDUP_BLOCKS, SYNTH_DEDUP_FILES = 0, 1, 2  # pfscdc.h PFSCDC_SYNTH_*
+
+
 @dataclass(frozen=True)
 class ChunkParams:
     """chunk.WithRollingHashConfig + WithMinMax (chunk/option.go:50-64); defaults writer.go:39-44."""
@@ -129,31 +132,61 @@ class Chunker:
         n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)
         return np.array(out[:min(n, cap)], dtype=np.uint64)
 
-    def fill_synthetic(self, tensor, file_offsets: Sequence[int], seed: int) -> None:
+    def fill_synthetic(self, tensor, file_offsets: Sequence[int], seed: int,
+                       mode: int = SYNTH_RANDOM) -> None:
         """Fill a torch uint8 CUDA tensor with the synthetic byte stream (see pfscdc.h)."""
         offs = _offsets_array(file_offsets)
-        rc = self.lib.pfscdc_fill_synthetic(self.ctx, tensor.data_ptr(),
-                                            offs.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                            len(offs) - 1, seed)
+        rc = self.lib.pfscdc_fill_synthetic_ex(self.ctx, tensor.data_ptr(),
+                                               offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                               len(offs) - 1, seed, mode)
         self._check(rc, "fill_synthetic")
 
 
-def synthetic_bytes(file_offsets: Sequence[int], seed: int) -> np.ndarray:
+_POOL_FILE = 1 << 23
+_M64 = (1 << 64) - 1
+
+
+def _mix64(x: int) -> int:
+    """murmur3 fmix64 (the dedup decision hash of pfscdc.h)."""
+    x &= _M64
+    x = ((x ^ (x >> 33)) * 0xFF51AFD7ED558CCD) & _M64
+    x = ((x ^ (x >> 33)) * 0xC4CEB9FE1A85EC53) & _M64
+    return x ^ (x >> 33)
+
+
+def _synth_words(fid: int, w0: int, nw: int, seed: int) -> np.ndarray:
+    gamma = np.uint64((seed + 1) * 0x9E3779B97F4A7C15 % (1 << 64))
+    with np.errstate(over="ignore"):
+        z = (np.uint64(fid) << np.uint64(40)) | np.arange(w0, w0 + nw, dtype=np.uint64)
+        z = z + gamma
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").view(np.uint8)
+
+
+def synthetic_bytes(file_offsets: Sequence[int], seed: int, mode: int = SYNTH_RANDOM) -> np.ndarray:
     """Host copy of the synthetic stream (same definition as the device generator)."""
     offs = np.asarray(file_offsets, dtype=np.uint64)
     out = np.empty(int(offs[-1]), dtype=np.uint8)
-    gamma = np.uint64((seed + 1) * 0x9E3779B97F4A7C15 % (1 << 64))
     for f in range(len(offs) - 1):
         a, b = int(offs[f]), int(offs[f + 1])
         n = b - a
         if n == 0:
             continue
-        nw = (n + 7) // 8
-        with np.errstate(over="ignore"):
-            z = (np.uint64(f) << np.uint64(40)) | np.arange(nw, dtype=np.uint64)
-            z = z + gamma
-            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-            z = z ^ (z >> np.uint64(31))
-        out[a:b] = z.astype("<u8").view(np.uint8)[:n]
+        if mode == SYNTH_DEDUP_FILES:
+            h = _mix64((seed << 48) ^ (f << 24) ^ 0x5EEDF11E)
+            fid = _POOL_FILE + ((h >> 1) & 63) if h & 1 else f
+            out[a:b] = _synth_words(fid, 0, (n + 7) // 8, seed)[:n]
+        elif mode == SYNTH_DEDUP_BLOCKS:
+            for k in range((n + (1 << 20) - 1) >> 20):
+                o0, o1 = k << 20, min(n, (k + 1) << 20)
+                h = _mix64((seed << 48) ^ (f << 24) ^ k ^ 0xC5C5C5C5)
+                if h & 1:
+                    words = _synth_words(_POOL_FILE + ((h >> 1) & 63), 0, (o1 - o0 + 7) // 8, seed)
+                else:
+                    words = _synth_words(f, o0 >> 3, (o1 - o0 + 7) // 8, seed)
+                out[a + o0:a + o1] = words[:o1 - o0]
+        else:
+            out[a:b] = _synth_words(f, 0, (n + 7) // 8, seed)[:n]
     return out

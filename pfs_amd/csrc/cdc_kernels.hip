@@ -985,8 +985,28 @@ PFS_DEV uint64_t synth_word(uint64_t f, uint64_t k, uint64_t seed) {
   return z ^ (z >> 31);
 }
 
+// Dedup-heavy layouts (BASELINE configs[4]): source (file, word) of the byte at offset o of
+// file f.  mode 1: each 1 MiB block of a file is, with p = 1/2, a copy of one of 64 pooled
+// blocks (pool "file" kPoolFile + id), else fresh bytes; mode 2: the same per whole file.
+constexpr uint64_t kPoolFile = 1ULL << 23;
+PFS_DEV uint64_t synth_mix(uint64_t x) {
+  x = (x ^ (x >> 33)) * 0xFF51AFD7ED558CCDULL;
+  x = (x ^ (x >> 33)) * 0xC4CEB9FE1A85EC53ULL;
+  return x ^ (x >> 33);
+}
+PFS_DEV uint64_t synth_byte_word(uint64_t f, uint64_t o, uint64_t seed, uint32_t mode) {
+  if (mode == 1) {
+    const uint64_t h = synth_mix((seed << 48) ^ (f << 24) ^ (o >> 20) ^ 0xC5C5C5C5ULL);
+    if (h & 1) return synth_word(kPoolFile + ((h >> 1) & 63), (o & 0xFFFFF) >> 3, seed);
+  } else if (mode == 2) {
+    const uint64_t h = synth_mix((seed << 48) ^ (f << 24) ^ 0x5EEDF11EULL);
+    if (h & 1) return synth_word(kPoolFile + ((h >> 1) & 63), o >> 3, seed);
+  }
+  return synth_word(f, o >> 3, seed);
+}
+
 __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ offs,
-                             uint32_t nfiles, uint64_t seed) {
+                             uint32_t nfiles, uint64_t seed, uint32_t mode) {
   const uint64_t n = offs[nfiles];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 8;
   for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; g < n; g += stride) {
@@ -1004,7 +1024,7 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
       if (p >= n) break;
       while (f + 1 < nfiles && offs[f + 1] <= p) f++;
       const uint64_t o = p - offs[f];
-      bytes[b] = (uint8_t)(synth_word(f, o >> 3, seed) >> (8 * (o & 7)));
+      bytes[b] = (uint8_t)(synth_byte_word(f, o, seed, mode) >> (8 * (o & 7)));
     }
     if (g + 8 <= n) {
       uint64_t w;
@@ -1103,8 +1123,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
 }
 
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
-                        hipStream_t st) {
-  synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, seed);
+                        uint32_t mode, hipStream_t st) {
+  synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, seed, mode);
   return hipGetLastError();
 }
 

@@ -395,9 +395,10 @@ void pfscdc_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
-int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
-                          uint32_t nfiles, uint64_t seed) {
+int pfscdc_fill_synthetic_ex(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
+                             uint32_t nfiles, uint64_t seed, uint32_t mode) {
   if (!c || !file_offsets || (!dev_bytes && nfiles && file_offsets[nfiles])) return PFSCDC_EINVAL;
+  if (mode > PFSCDC_SYNTH_DEDUP_FILES) return PFSCDC_EINVAL;
   if (nfiles == 0 || file_offsets[nfiles] == 0) return PFSCDC_OK;
   HIP_OK(c, hipSetDevice(c->device));
   HIP_OK(c, c->h_offs.ensure(nfiles + 1));
@@ -405,9 +406,14 @@ int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_o
   std::memcpy(c->h_offs.p, file_offsets, sizeof(uint64_t) * (nfiles + 1));
   HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (nfiles + 1),
                            hipMemcpyHostToDevice, c->stream));
-  HIP_OK(c, launch_synth((uint8_t*)dev_bytes, c->d_offs.p, nfiles, seed, c->stream));
+  HIP_OK(c, launch_synth((uint8_t*)dev_bytes, c->d_offs.p, nfiles, seed, mode, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   return PFSCDC_OK;
+}
+
+int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
+                          uint32_t nfiles, uint64_t seed) {
+  return pfscdc_fill_synthetic_ex(c, dev_bytes, file_offsets, nfiles, seed, PFSCDC_SYNTH_RANDOM);
 }
 
 }  // extern "C"

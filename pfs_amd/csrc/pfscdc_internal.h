@@ -62,6 +62,6 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st);
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
-                        hipStream_t st);
+                        uint32_t mode, hipStream_t st);
 
 }  // namespace pfscdc
