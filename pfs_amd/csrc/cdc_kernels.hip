@@ -685,6 +685,66 @@ PFS_DEV uint64_t perm_add(uint64_t c, uint64_t d) {
     b = xor_rotr63(b, c);              \
   } while (0)
 
+// One BLAKE2b round of the quad kernel in hand-scheduled gfx950 assembly.  The state lives
+// in fixed registers a = v[100:101], b = v[102:103], c = v[104:105], d = v[106:107] (temps
+// v108-v111) so 64-bit ops (v_lshl_add_u64) and their 32-bit halves (DPP, alignbit) can be
+// named; the compiler-scheduled form spends ~26 VALU per G on register-pair copies and
+// separate DPP moves.  Here each G is 22 VALU: the incoming quad rotation of b, c and d is
+// a DPP source operand of their first uses (v_add_co_u32_dpp / v_addc_co_u32_dpp for
+// a + b' and c' + d, v_xor_b32_dpp for d' ^ a and b' ^ c), so nothing is moved.
+// Hazards: a DPP read needs 2 wait states after the VALU write of its source; inside a G
+// the closest pair is b (written by the last two instructions of the previous G, read by
+// instructions 2-3), covered by the a + x add in between; each round starts with s_nop 1
+// for whatever the compiler placed before it.
+#define PFS_DPP(P) " quad_perm:" P " row_mask:0xf bank_mask:0xf\n"
+#define PFS_G_ASM(PB, PC, PD, X, Y)                                    \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, " X "\n"                  \
+  "v_add_co_u32_dpp v100, vcc, v102, v100" PFS_DPP(PB)                 \
+  "v_addc_co_u32_dpp v101, vcc, v103, v101, vcc" PFS_DPP(PB)           \
+  "v_xor_b32_dpp v108, v107, v101" PFS_DPP(PD)                         \
+  "v_xor_b32_dpp v109, v106, v100" PFS_DPP(PD)                         \
+  "v_add_co_u32_dpp v104, vcc, v104, v108" PFS_DPP(PC)                 \
+  "v_addc_co_u32_dpp v105, vcc, v105, v109, vcc" PFS_DPP(PC)           \
+  "v_xor_b32_dpp v110, v102, v104" PFS_DPP(PB)                         \
+  "v_xor_b32_dpp v111, v103, v105" PFS_DPP(PB)                         \
+  "v_alignbit_b32 v102, v111, v110, 24\n"                              \
+  "v_alignbit_b32 v103, v110, v111, 24\n"                              \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, " Y "\n"                  \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"             \
+  "v_xor_b32 v110, v108, v100\n"                                       \
+  "v_xor_b32 v111, v109, v101\n"                                       \
+  "v_alignbit_b32 v106, v111, v110, 16\n"                              \
+  "v_alignbit_b32 v107, v110, v111, 16\n"                              \
+  "v_lshl_add_u64 v[104:105], v[104:105], 0, v[106:107]\n"             \
+  "v_xor_b32 v110, v102, v104\n"                                       \
+  "v_xor_b32 v111, v103, v105\n"                                       \
+  "v_alignbit_b32 v102, v110, v111, 31\n"                              \
+  "v_alignbit_b32 v103, v111, v110, 31\n"
+#define PFS_QP_ID "[0,1,2,3]"
+#define PFS_QP_R1 "[1,2,3,0]"  // 0x39: lane j reads lane j+1
+#define PFS_QP_R2 "[2,3,0,1]"  // 0x4E
+#define PFS_QP_R3 "[3,0,1,2]"  // 0x93
+// column G (its b, c, d arrive in the previous diagonal layout: undo it on first use), then
+// diagonal G (b <- lane j+1, c <- j+2, d <- j+3)
+#define PFS_ROUND_ASM(PB0, PC0, PD0)                                          \
+  "s_nop 1\n" PFS_G_ASM(PB0, PC0, PD0, "%[x0]", "%[x1]")                      \
+      PFS_G_ASM(PFS_QP_R1, PFS_QP_R2, PFS_QP_R3, "%[x2]", "%[x3]")
+#define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                            \
+  do {                                                                                  \
+    if (FIRST)                                                                          \
+      asm volatile(PFS_ROUND_ASM(PFS_QP_ID, PFS_QP_ID, PFS_QP_ID)                      \
+                   : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c),        \
+                     "+{v[106:107]}"(d)                                                 \
+                   : [x0] "v"(x0_), [x1] "v"(x1_), [x2] "v"(x2_), [x3] "v"(x3_)          \
+                   : "vcc", "v108", "v109", "v110", "v111");                            \
+    else                                                                                \
+      asm volatile(PFS_ROUND_ASM(PFS_QP_R3, PFS_QP_R2, PFS_QP_R1)                      \
+                   : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c),        \
+                     "+{v[106:107]}"(d)                                                 \
+                   : [x0] "v"(x0_), [x1] "v"(x1_), [x2] "v"(x2_), [x3] "v"(x3_)          \
+                   : "vcc", "v108", "v109", "v110", "v111");                            \
+  } while (0)
+
 __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
@@ -788,6 +848,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
         y2 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][2]);
         y3 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][3]);
       }
+#ifdef PFS_HASH_CXX
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
       c = quad_perm64<0x4E>(c);            // c <- v[8+(j+2)%4]
       d = quad_perm64<0x93>(d);            // d <- v[12+(j+3)%4]
@@ -796,12 +857,20 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
       c = quad_perm64<0x4E>(c);
       d = quad_perm64<0x39>(d);
       b = quad_perm64<0x93>(b);
+#else
+      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves b, c, d in the diagonal layout
+#endif
       x0 = y0; x1 = y1; x2 = y2; x3 = y3;
       if (r == 5 && active && !last) {  // block blk+1 -> the other buffer; fetch blk+2
         lds_put(nxt);
         if (blk + 2 < nblk) load_block(blk + 2);
       }
     }
+#ifndef PFS_HASH_CXX
+    c = quad_perm64<0x4E>(c);  // back to the column layout
+    d = quad_perm64<0x39>(d);
+    b = quad_perm64<0x93>(b);
+#endif
     ha ^= a ^ c;
     hb ^= b ^ d;
     if (active) {
