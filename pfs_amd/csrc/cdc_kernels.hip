@@ -524,14 +524,19 @@ __global__ __launch_bounds__(kCompactBlock) void segcompact_kernel(
 // 5. BLAKE2b-256 per segment, 4 lanes per segment
 // ------------------------------------------------------------------------------------------
 
-__constant__ uint64_t kB2IV[8] = {
+constexpr uint64_t kB2IV[8] = {
     0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
     0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
     0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 
+template <typename T>
+PFS_DEV T pick4(uint32_t j, T v0, T v1, T v2, T v3) {
+  return j == 0 ? v0 : j == 1 ? v1 : j == 2 ? v2 : v3;
+}
+
 // Per (round, lane): byte offsets (word*8) of the 4 message words the lane consumes:
 // column G_j uses sigma[r][2j], sigma[r][2j+1]; diagonal G_{4+j} uses sigma[r][8+2j], [9+2j].
-__constant__ uint32_t kSigmaPack[12][4] = {
+constexpr uint32_t kSigmaPack[12][4] = {
 #define PK(a, b, c, d) ((uint32_t)(a) * 8u | (uint32_t)(b) * 8u << 8 | (uint32_t)(c) * 8u << 16 | (uint32_t)(d) * 8u << 24)
 #define ROW(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
   {PK(s0, s1, s8, s9), PK(s2, s3, s10, s11), PK(s4, s5, s12, s13), PK(s6, s7, s14, s15)}
@@ -770,14 +775,16 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   uint32_t ma[12][4];
 #pragma unroll
   for (int r = 0; r < 12; r++) {
-    const uint32_t pk = kSigmaPack[r][j];
+    const uint32_t pk = pick4(j, kSigmaPack[r][0], kSigmaPack[r][1], kSigmaPack[r][2], kSigmaPack[r][3]);
 #pragma unroll
     for (int k = 0; k < 4; k++) ma[r][k] = slot + ((pk >> (8 * k)) & 0xFFu);
   }
-  const uint64_t iv_c = kB2IV[j];
-  const uint64_t iv_d = kB2IV[4 + j];
-  const uint64_t h0a = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : kB2IV[j];  // digest 32, fanout/depth 1
-  const uint64_t h0b = kB2IV[4 + j];
+  // lane constants from immediates (v_cndmask), not loads: a load here would leave the
+  // compiler unable to count vmcnt across the loop and it waits for vmcnt(0) every block
+  const uint64_t iv_c = pick4(j, kB2IV[0], kB2IV[1], kB2IV[2], kB2IV[3]);
+  const uint64_t iv_d = pick4(j, kB2IV[4], kB2IV[5], kB2IV[6], kB2IV[7]);
+  const uint64_t h0a = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : iv_c;  // digest 32, fanout/depth 1
+  const uint64_t h0b = iv_d;
 
   bool active = false;   // this quad holds a segment
   bool drained = false;  // wave-uniform: the queue is exhausted
