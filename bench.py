@@ -52,6 +52,9 @@ def parse():
                     help="c2: configs[1] batches per step (one launch group, resident in HBM "
                          "together)")
     ap.add_argument("--dedup", default="blocks", choices=["blocks", "files"], help="c5 layout")
+    ap.add_argument("--ref-ids", action="store_true",
+                    help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
+                         "§8 next row 1) inside the step")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="steps in flight (one GPU context + input buffer each)")
@@ -168,7 +171,7 @@ def main():
     sbytes = int(offs[sfiles])
 
     S = max(1, args.inflight)
-    chunkers = [Chunker(params, device=local) for _ in range(S)]
+    chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
     batches = []
     for k in range(S):
         t = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -179,6 +182,8 @@ def main():
     gather = world > 1 or args.config == "c5"
     torch.cuda.synchronize()
     acc = {"scan": 0.0, "compact": 0.0, "select": 0.0, "hash": 0.0, "total": 0.0}
+    if args.ref_ids:
+        acc["ref_ids"] = 0.0
     pending = [False] * S
     last = {}
 
@@ -240,6 +245,9 @@ def main():
     dom = "hash" if avg["hash"] >= avg["scan"] else "scan"
     roofline = roof(avg[dom])
     roofline["kernel"] = {"hash": "blake2b_kernel", "scan": "cdc_scan_kernel"}[dom]
+    if args.ref_ids and avg["ref_ids"] > avg[dom]:
+        roofline = roof(avg["ref_ids"])
+        roofline["kernel"] = "blake2b_kernel<true> (ChaCha20 + BLAKE2b of the ciphertext)"
     roofline_cdc = roof(avg["scan"])
     roofline_cdc["kernel"] = "cdc_scan_kernel"
     if args.traffic_json and os.path.exists(args.traffic_json):
@@ -258,6 +266,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)",
+        "ref_ids": bool(args.ref_ids),
         "config": info,
         "segments_per_step": int(len(res.segments)),
         "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
@@ -336,6 +345,16 @@ def main():
                                            ("offset", "size", "file", "flags", "hash"))
         out["parity"] = {"gpu_equals_cpu_oracle": bool(same), "segments": int(len(segs)),
                          "checked": "the cpu_baseline sample, last measured step"}
+        if args.ref_ids:
+            nchk = min(16, len(g))
+            ok = True
+            for i in np.linspace(0, len(g) - 1, nchk).astype(int):
+                sg = g[i]
+                a = int(offs[sg["file"]]) + int(sg["offset"])
+                rid, dek = och.create_ref_id(hdata[a:a + int(sg["size"])].tobytes())
+                ok &= bytes(res.refs[i]["id"]) == rid and bytes(res.refs[i]["dek"]) == dek
+            out["parity"]["ref_ids_equal_oracle"] = bool(ok)
+            out["parity"]["ref_ids_checked"] = int(nchk)
         if args.config == "c5" and "index" in last:
             # the oracle's digests of the sample give the same hit rate as the GPU's
             ref = local_index(segs, fbase)

@@ -49,6 +49,16 @@ typedef struct pfscdc_segment {
   uint8_t hash[32]; /* BLAKE2b-256 (pachhash.Sum, pachhash/hash.go:27-30) */
 } pfscdc_segment;   /* 56 bytes */
 
+/* Ref of the chunk a segment forms when each file is its own writer (the batch form): what
+ * chunk.Create(ctx, CreateOptions{}, chunk, ...) stores (transform.go:26-46, client.go:57).
+ * CreateOptions{} means no compression and an empty secret, so
+ *   dek = BLAKE2b-256(BLAKE2b-256(chunk))      (deriveKey, transform.go:173-178)
+ *   id  = BLAKE2b-256(ChaCha20_dek,nonce0(chunk)) (cryptoXOR :181-188, then Hash) */
+typedef struct pfscdc_ref {
+  uint8_t id[32];  /* Ref.Id */
+  uint8_t dek[32]; /* Ref.Dek */
+} pfscdc_ref;
+
 #define PFSCDC_SEG_VALID 1u
 #define PFSCDC_SEG_CUT 2u /* the segment ends on a CDC cut (else: at end of file) */
 
@@ -92,6 +102,16 @@ int pfscdc_wait(pfscdc_ctx* ctx);
 uint64_t pfscdc_num_segments(const pfscdc_ctx* ctx);
 const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* ctx);
 const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* ctx);
+
+/* Options of every following scan on ctx (bit set).  PFSCDC_OPT_REF_IDS: also compute each
+ * segment's pfscdc_ref (a second BLAKE2b pass over the ChaCha20 ciphertext, fused). */
+#define PFSCDC_OPT_REF_IDS 1u
+int pfscdc_set_options(pfscdc_ctx* ctx, uint32_t options);
+/* Refs of the last completed scan, aligned with pfscdc_segments (NULL unless the scan ran
+ * with PFSCDC_OPT_REF_IDS). */
+const pfscdc_ref* pfscdc_refs(const pfscdc_ctx* ctx);
+/* Device time (ms) of the last scan's Ref.Id kernels (0 without PFSCDC_OPT_REF_IDS). */
+int pfscdc_last_ref_ms(pfscdc_ctx* ctx, float* ms);
 
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
  * positions inside dense tiles are reported through the tile marker instead.  Debug/test

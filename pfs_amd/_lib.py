@@ -23,6 +23,7 @@ PFSCDC_ECALLBACK = -6
 
 SEG_VALID = 1
 SEG_CUT = 2
+OPT_REF_IDS = 1
 
 # Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -30,6 +31,7 @@ EXPORTED = [
     "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
+    "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms",
     "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
     "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
@@ -65,8 +67,18 @@ assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32
 WRITER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(ChunkRef), C.POINTER(AnnotationOut),
                         C.c_uint32)
 
-# numpy view of pfscdc_segment
+# numpy views of pfscdc_segment / pfscdc_ref
 SEGMENT_DTYPE = None
+REF_DTYPE = None
+
+
+def ref_dtype():
+    global REF_DTYPE
+    if REF_DTYPE is None:
+        import numpy as np
+        REF_DTYPE = np.dtype([("id", "u1", (32,)), ("dek", "u1", (32,))])
+        assert REF_DTYPE.itemsize == 64
+    return REF_DTYPE
 
 
 def segment_dtype():
@@ -125,6 +137,9 @@ def load() -> C.CDLL:
             "pfscdc_file_segment_begin": (P(u64), [vp]),
             "pfscdc_debug_candidates": (u64, [vp, P(u64), u64]),
             "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
+            "pfscdc_set_options": (i32, [vp, u32]),
+            "pfscdc_refs": (vp, [vp]),
+            "pfscdc_last_ref_ms": (i32, [vp, P(C.c_float)]),
             "pfscdc_host_alloc": (vp, [u64]),
             "pfscdc_host_free": (None, [vp]),
             "pfscdc_fill_synthetic": (i32, [vp, vp, P(u64), u32, u64]),

@@ -36,6 +36,7 @@ class ScanResult:
     segments: np.ndarray        # structured SEGMENT_DTYPE, ordered by (file, offset)
     file_begin: np.ndarray      # uint64[nfiles+1]: file f owns segments[file_begin[f]:file_begin[f+1]]
     timings_ms: Optional[dict] = None
+    refs: Optional[np.ndarray] = None  # REF_DTYPE (id, dek) per segment with ref_ids=True
 
     def file_segments(self, f: int) -> np.ndarray:
         return self.segments[int(self.file_begin[f]):int(self.file_begin[f + 1])]
@@ -51,7 +52,8 @@ def _offsets_array(file_offsets: Sequence[int]) -> np.ndarray:
 class Chunker:
     """A GPU context bound to one device and one parameter set."""
 
-    def __init__(self, params: ChunkParams = ChunkParams(), device: int = 0):
+    def __init__(self, params: ChunkParams = ChunkParams(), device: int = 0,
+                 ref_ids: bool = False):
         self.lib = _lib.load()
         self.params = params
         self.device = device
@@ -61,6 +63,15 @@ class Chunker:
         if rc:
             raise _lib.PfsCdcError(rc, "pfscdc_ctx_create failed (no GPU or bad params)")
         self.ctx = ctx
+        self.ref_ids = False
+        if ref_ids:
+            self.set_ref_ids(True)
+
+    def set_ref_ids(self, on: bool) -> None:
+        """Also compute each segment's Ref (Id, Dek) of chunk.Create (pfscdc.h)."""
+        self._check(self.lib.pfscdc_set_options(self.ctx, _lib.OPT_REF_IDS if on else 0),
+                    "set_options")
+        self.ref_ids = on
 
     def close(self) -> None:
         if getattr(self, "ctx", None):
@@ -116,7 +127,13 @@ class Chunker:
         bp = self.lib.pfscdc_file_segment_begin(self.ctx)
         begin = np.ctypeslib.as_array(bp, shape=(self._nfiles + 1,)).copy() if bp else \
             np.zeros(self._nfiles + 1, dtype=np.uint64)
-        return ScanResult(segs, begin)
+        refs = None
+        if self.ref_ids:
+            rdt = _lib.ref_dtype()
+            rp = self.lib.pfscdc_refs(self.ctx)
+            refs = np.frombuffer(C.string_at(rp, n * rdt.itemsize), dtype=rdt).copy() \
+                if (n and rp) else np.zeros(0, dtype=rdt)
+        return ScanResult(segs, begin, refs=refs)
 
     def scan(self, data, file_offsets: Sequence[int]) -> ScanResult:
         self.scan_async(data, file_offsets)
@@ -125,7 +142,12 @@ class Chunker:
     def timings(self) -> dict:
         out = (C.c_float * 5)()
         self._check(self.lib.pfscdc_last_timings(self.ctx, out), "timings")
-        return dict(zip(["scan", "compact", "select", "hash", "total"], list(out)))
+        t = dict(zip(["scan", "compact", "select", "hash", "total"], list(out)))
+        if self.ref_ids:
+            ms = C.c_float()
+            self._check(self.lib.pfscdc_last_ref_ms(self.ctx, C.byref(ms)), "timings")
+            t["ref_ids"] = ms.value
+        return t
 
     def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
         out = (C.c_uint64 * cap)()

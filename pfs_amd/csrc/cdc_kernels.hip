@@ -690,6 +690,64 @@ PFS_DEV uint64_t perm_add(uint64_t c, uint64_t d) {
     b = xor_rotr63(b, c);              \
   } while (0)
 
+// ChaCha20 block (RFC 8439 §2.3; x/crypto chacha20 with a zero 12-byte nonce) computed by a
+// quad: lane j holds column j (a = const[j], b = key[j], c = key[4+j], d = counter or 0),
+// the diagonal round rotates b, c, d across the quad.  ks[w] = keystream word j + 4w.
+PFS_DEV uint32_t rotl32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+template <int CTRL>
+PFS_DEV uint32_t qp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
+}
+#define PFS_QR(a, b, c, d)                 \
+  do {                                     \
+    a += b; d ^= a; d = rotl32(d, 16);     \
+    c += d; b ^= c; b = rotl32(b, 12);     \
+    a += b; d ^= a; d = rotl32(d, 8);      \
+    c += d; b ^= c; b = rotl32(b, 7);      \
+  } while (0)
+PFS_DEV void chacha20_column(uint32_t (&ks)[4], uint32_t a0, uint32_t b0, uint32_t c0,
+                             uint32_t d0) {
+  uint32_t a = a0, b = b0, c = c0, d = d0;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    PFS_QR(a, b, c, d);  // column round
+    b = qp32<0x39>(b);   // b <- column j+1, c <- j+2, d <- j+3
+    c = qp32<0x4E>(c);
+    d = qp32<0x93>(d);
+    PFS_QR(a, b, c, d);  // diagonal round
+    b = qp32<0x93>(b);
+    c = qp32<0x4E>(c);
+    d = qp32<0x39>(d);
+  }
+  ks[0] = a + a0;
+  ks[1] = b + b0;
+  ks[2] = c + c0;
+  ks[3] = d + d0;
+}
+
+// One BLAKE2b-256 compression in one lane (message m[16], counter t, last-block flag).
+PFS_DEV void b2_compress_lane(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t, bool last);
+
+// Ref.Dek per segment: BLAKE2b-256(secret || DataRef.Hash) with the empty secret of
+// CreateOptions{} (transform.go:173-178): a single 32-byte block.  One lane per segment.
+__global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
+                           const uint64_t* __restrict__ seg_count, pfscdc_ref* __restrict__ refs,
+                           uint32_t* __restrict__ counter) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *counter = 0;  // the Ref.Id launch's queue (same LPT order as the hash)
+  if (i >= *seg_count) return;
+  uint64_t m[16];
+  const uint64_t* hs = reinterpret_cast<const uint64_t*>(segs[i].hash);
+#pragma unroll
+  for (int k = 0; k < 16; k++) m[k] = k < 4 ? hs[k] : 0;
+  uint64_t h[8] = {kB2IV[0] ^ 0x01010020ULL, kB2IV[1], kB2IV[2], kB2IV[3],
+                   kB2IV[4], kB2IV[5], kB2IV[6], kB2IV[7]};
+  b2_compress_lane(h, m, 32, true);
+  uint64_t* out = reinterpret_cast<uint64_t*>(refs[i].dek);
+#pragma unroll
+  for (int k = 0; k < 4; k++) out[k] = h[k];
+}
+
 // One BLAKE2b round of the quad kernel in hand-scheduled gfx950 assembly.  The state lives
 // in fixed registers a = v[100:101], b = v[102:103], c = v[104:105], d = v[106:107] (temps
 // v108-v111) so 64-bit ops (v_lshl_add_u64) and their 32-bit halves (DPP, alignbit) can be
@@ -750,10 +808,18 @@ PFS_DEV uint64_t perm_add(uint64_t c, uint64_t d) {
                    : "vcc", "v108", "v109", "v110", "v111");                            \
   } while (0)
 
+// CIPHER = false: DataRef.Hash = BLAKE2b-256(segment) into segs[].hash.
+// CIPHER = true:  Ref.Id = BLAKE2b-256(ChaCha20_dek(segment)) into refs[].id, dek read from
+// refs[].dek (chunk.Create with CreateOptions{}: transform.go:26-46,173-188, client.go:57).
+// The keystream for the two 64-byte ChaCha20 blocks of each 128-byte message block is
+// computed by the same quad (lane j = state column j, DPP diagonals, as for BLAKE2b) and
+// XORed into the LDS message buffer (ds_xor_b32) before the BLAKE2b rounds read it.
+template <bool CIPHER>
 __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
-    const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes) {
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
+    pfscdc_ref* __restrict__ refs) {
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
   // i&1 while the quad's next block (loaded into registers one iteration earlier) is written
   // to the other buffer halfway through; the wave-uniform parity makes every ds_read offset
@@ -791,8 +857,11 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   uint64_t L = 0, nblk = 0, blk = 0;
   const uint8_t* src = data;
   pfscdc_segment* seg = segs;
+  uint32_t sidx = 0;
   uint64_t ha = 0, hb = 0;
   uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;  // the quad's block blk+1 (lane j: bytes 32j..)
+  uint32_t key_b = 0, key_c = 0;  // CIPHER: ChaCha20 key words j and 4+j (state b, c of column j)
+  const uint32_t cc_a = pick4(j, 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u);
 
   auto lds_put = [&](uint32_t buf) {
     reinterpret_cast<uint4*>(my + buf)[0] = m0;
@@ -819,8 +888,14 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
           const uint64_t below = want & ((1ULL << (lane & ~3u)) - 1);
           const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(below);
           if (idx < nseg) {
-            seg = segs + order[idx];
+            sidx = order[idx];
+            seg = segs + sidx;
             L = seg->size;
+            if (CIPHER) {
+              const uint32_t* dk = reinterpret_cast<const uint32_t*>(refs[sidx].dek);
+              key_b = dk[j];
+              key_c = dk[4 + j];
+            }
             src = data + offs[seg->file] + seg->offset;
             nblk = L == 0 ? 1 : (L + 127) / 128;
             blk = 0;
@@ -838,6 +913,25 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
 
     const bool last = blk + 1 == nblk;
+    if (CIPHER) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // keystream blocks 2*blk and 2*blk+1, XORed into the plaintext already in LDS; in the
+      // last block only the bytes before the segment end (BLAKE2b zero-pads the rest)
+      const int64_t avail = (int64_t)(L - blk * 128);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint32_t ks[4];
+        chacha20_column(ks, cc_a, key_b, key_c, j == 0 ? (uint32_t)(2 * blk + h) : 0u);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_msg + cur + slot + 64 * h) + j;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const uint32_t v = last ? ks[w] & keep_bytes(avail - 64 * h - 16 * w - 4 * (int64_t)j) : ks[w];
+          __hip_atomic_fetch_xor(dst + 4 * w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -883,7 +977,8 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     if (active) {
       blk++;
       if (last) {  // digest = h[0..3] little endian; lane j owns h[j]
-        reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
+        if (CIPHER) reinterpret_cast<uint64_t*>(refs[sidx].id)[j] = ha;
+        else reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
         active = false;
       }
     }
@@ -918,6 +1013,30 @@ constexpr uint8_t kSigma[12][16] = {
 constexpr uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                              0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                              0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+PFS_DEV void b2_compress_lane(uint64_t (&h)[8], const uint64_t (&x)[16], uint64_t t, bool last) {
+  uint64_t v[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    v[i] = h[i];
+    v[8 + i] = kIV[i];
+  }
+  v[12] ^= t;
+  v[14] ^= last ? ~0ULL : 0ULL;
+#pragma unroll
+  for (int r = 0; r < 12; r++) {
+    PFS_G(v[0], v[4], v[8], v[12], x[kSigma[r][0]], x[kSigma[r][1]]);
+    PFS_G(v[1], v[5], v[9], v[13], x[kSigma[r][2]], x[kSigma[r][3]]);
+    PFS_G(v[2], v[6], v[10], v[14], x[kSigma[r][4]], x[kSigma[r][5]]);
+    PFS_G(v[3], v[7], v[11], v[15], x[kSigma[r][6]], x[kSigma[r][7]]);
+    PFS_G(v[0], v[5], v[10], v[15], x[kSigma[r][8]], x[kSigma[r][9]]);
+    PFS_G(v[1], v[6], v[11], v[12], x[kSigma[r][10]], x[kSigma[r][11]]);
+    PFS_G(v[2], v[7], v[8], v[13], x[kSigma[r][12]], x[kSigma[r][13]]);
+    PFS_G(v[3], v[4], v[9], v[14], x[kSigma[r][14]], x[kSigma[r][15]]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
+}
 
 // One 128-byte block for this lane: eight 16-byte loads.
 PFS_DEV void blk_load_full(uint4 (&m)[8], const uint8_t* p) {
@@ -1175,7 +1294,6 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st) {
   if (max_segments == 0) return hipSuccess;
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
-  // resident waves: kHashWavesPerSimd per SIMD (4 SIMDs per CU), no more than the segments need
   static const int waves_per_simd = [] {  // tuning knob (PFSCDC_HASH_WAVES), default 2
     const char* e = getenv("PFSCDC_HASH_WAVES");
     const int w = e ? atoi(e) : kHashWavesPerSimd;
@@ -1191,10 +1309,25 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   }
   const uint64_t quads_per_block = kHashBlock / 4;
   const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
+  const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashBlock / 64);
+  const uint64_t grid = need < full ? need : full;
+  blake2b_kernel<false><<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order,
+                                                               counter, nbytes, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
+                          const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
+                          uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
+                          hipStream_t st) {
+  if (max_segments == 0) return hipSuccess;
+  dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
+  const uint64_t quads_per_block = kHashBlock / 4;
+  const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
   const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order, counter,
-                                                     nbytes);
+  blake2b_kernel<true><<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order,
+                                                              counter, nbytes, refs);
   return hipGetLastError();
 }
 

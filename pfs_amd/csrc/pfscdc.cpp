@@ -78,9 +78,13 @@ struct pfscdc_ctx {
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
+  DevBuf<pfscdc_ref> d_refs;
+  PinnedBuf<pfscdc_ref> h_refs;
+  uint32_t options = 0;
+  bool have_refs = false;
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
   PinnedBuf<pfscdc_segment> h_segs;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[8] = {};
   bool pending = false;
   uint32_t nfiles = 0;
   uint64_t nbytes = 0;
@@ -213,6 +217,8 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_segs.release();
   c->d_order.release();
   c->d_qctr.release();
+  c->d_refs.release();
+  c->h_refs.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -273,7 +279,8 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, c->d_slots.ensure(cap));
   HIP_OK(c, c->d_segs.ensure(cap));
   HIP_OK(c, c->d_order.ensure(cap));
-  HIP_OK(c, c->d_qctr.ensure(1));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  if (c->options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
@@ -322,6 +329,11 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
+  c->have_refs = (c->options & PFSCDC_OPT_REF_IDS) != 0;
+  if (c->have_refs && nfiles)
+    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
+                             c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, st));
+  HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)
     HIP_OK(c, hipMemcpyAsync(c->h_seg_begin.p, c->d_seg_begin.p, sizeof(uint64_t) * (nfiles + 1),
@@ -344,6 +356,12 @@ int pfscdc_wait(pfscdc_ctx* c) {
   if (total)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, total * sizeof(pfscdc_segment),
                              hipMemcpyDeviceToHost, c->stream));
+  if (c->have_refs) {
+    HIP_OK(c, c->h_refs.ensure(total));
+    if (total)
+      HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, total * sizeof(pfscdc_ref),
+                               hipMemcpyDeviceToHost, c->stream));
+  }
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->nsegs = total;
@@ -358,6 +376,24 @@ int pfscdc_scan(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_
 }
 
 uint64_t pfscdc_num_segments(const pfscdc_ctx* c) { return c ? c->nsegs : 0; }
+
+int pfscdc_set_options(pfscdc_ctx* c, uint32_t options) {
+  if (!c || (options & ~PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "set_options during a pending scan");
+  c->options = options;
+  return PFSCDC_OK;
+}
+
+const pfscdc_ref* pfscdc_refs(const pfscdc_ctx* c) {
+  return c && c->have_refs && !c->pending ? c->h_refs.p : nullptr;
+}
+
+int pfscdc_last_ref_ms(pfscdc_ctx* c, float* ms) {
+  if (!c || !ms) return PFSCDC_EINVAL;
+  *ms = 0.f;
+  if (c->have_refs) HIP_OK(c, hipEventElapsedTime(ms, c->ev[4], c->ev[6]));
+  return PFSCDC_OK;
+}
 const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* c) { return c ? c->h_segs.p : nullptr; }
 const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* c) {
   return c ? c->h_seg_begin.p : nullptr;

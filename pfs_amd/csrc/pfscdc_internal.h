@@ -40,6 +40,7 @@ struct TileRec {
 };
 static_assert(sizeof(TileRec) == 64, "tile record is one 64-byte line");
 static_assert(sizeof(pfscdc_segment) == 56, "segment record layout");
+static_assert(sizeof(pfscdc_ref) == 64, "ref record layout");
 
 void generate_hashes(int64_t seed, uint64_t out[256]);
 const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
@@ -61,6 +62,10 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st);
+hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
+                          const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
+                          uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
+                          hipStream_t st);
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
                         uint32_t mode, hipStream_t st);
 

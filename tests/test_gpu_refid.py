@@ -1,0 +1,68 @@
+"""GPU parity of the next §8 row: Ref.Id / Ref.Dek of chunk.Create with CreateOptions{}
+(/root/reference/src/internal/storage/chunk/transform.go:26-46,173-188; client.go:57):
+dek = BLAKE2b-256(BLAKE2b-256(chunk)), id = BLAKE2b-256(ChaCha20_dek(chunk)).
+
+The oracle (oracle/chunker.py create_ref_id, ChaCha20 pinned by RFC 8439 vectors in the CPU
+suite) is applied to every segment the GPU produced; the batch form treats each file as its
+own writer, so every segment is one chunk."""
+import numpy as np
+import pytest
+
+from oracle import chunker as Ch
+from oracle import coracle
+from pfs_amd.cdc import ChunkParams, Chunker, synthetic_bytes
+
+pytestmark = pytest.mark.gpu
+
+SMALL = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+
+
+def check_refs(res, data, offs, nmax=None):
+    assert res.refs is not None and len(res.refs) == len(res.segments)
+    idx = range(len(res.segments)) if nmax is None else \
+        np.linspace(0, len(res.segments) - 1, nmax).astype(int)
+    for i in idx:
+        s = res.segments[i]
+        a = int(offs[s["file"]]) + int(s["offset"])
+        chunk = data[a:a + int(s["size"])].tobytes()
+        rid, dek = Ch.create_ref_id(chunk)
+        assert bytes(res.refs[i]["dek"]) == dek, f"dek differs at segment {i}"
+        assert bytes(res.refs[i]["id"]) == rid, f"id differs at segment {i} (size {len(chunk)})"
+
+
+def test_ref_ids_small_segments_all_tail_shapes():
+    # sizes 1..30000 B: partial ChaCha blocks, partial BLAKE2b blocks, exact multiples
+    rng = np.random.default_rng(5)
+    lens = np.concatenate([np.arange(1, 200), [63, 64, 65, 127, 128, 129, 191, 192, 193, 255,
+                                                256, 257], rng.integers(1, 60_000, 150)])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 77)
+    c = Chunker(ChunkParams(SMALL.average_bits, SMALL.seed, SMALL.min, SMALL.max), 0, ref_ids=True)
+    res = c.scan(data, offs)
+    segs, _ = coracle.segment_files(data, offs, SMALL, nthreads=8)
+    assert np.array_equal(res.segments["hash"], segs["hash"])
+    check_refs(res, data, offs)
+
+
+def test_ref_ids_default_params_multi_mib():
+    offs = np.array([0, 3 << 20, (3 << 20) + 12345, (12 << 20) + 7, (40 << 20) + 999],
+                    dtype=np.uint64)
+    data = synthetic_bytes(offs, 11)
+    c = Chunker(ChunkParams(), 0, ref_ids=True)
+    res = c.scan(data, offs)
+    check_refs(res, data, offs)
+
+
+def test_ref_ids_device_resident_batch_and_toggle():
+    import torch
+    offs = (np.arange(65, dtype=np.uint64) * np.uint64(1_500_001))
+    c = Chunker(ChunkParams(), 0)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c.fill_synthetic(t, offs, 0xC2)
+    plain = c.scan(t, offs)
+    assert plain.refs is None
+    c.set_ref_ids(True)
+    res = c.scan(t, offs)
+    assert np.array_equal(res.segments, plain.segments)  # refs do not disturb the records
+    check_refs(res, t.cpu().numpy(), offs, nmax=24)
+    assert c.timings()["ref_ids"] > 0
