@@ -217,6 +217,67 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
                    mask64, table, s_count, s_cand);                                       \
   }
 
+// --- narrow masks (average_bits <= 32): the rolling hash without the outgoing byte -----------
+// With g_i = rotl(g_{i-1}, 1) ^ T[x_i] (the hash of everything since a start point), and the
+// rotation taken mod 64, h_i = g_i ^ rotl(g_{i-64}, 64) = g_i ^ g_{i-64}: bytes older than the
+// window cancel.  So the scan needs one table lookup per byte (T[in]) instead of two, and
+// the cut test (h_i & mask) == 0 only needs the low word of g_{i-64}: a 64-entry register
+// ring, indexed statically inside the unrolled 64-byte block.  The test itself is one
+// v_bitop3_b32: key = (g_lo ^ ring[t]) & mask.
+
+// Rare path for the g-form: rebuild h_{pos-1} from the 64 bytes before pos (zeros before the
+// stream start = the reset window), then re-roll the block exactly like record_block.
+PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail,
+                            uint64_t n_main, uint64_t pos, uint64_t n, uint64_t tile_base,
+                            uint64_t mask64, const uint64_t* __restrict__ table,
+                            uint32_t* s_count, uint32_t* s_cand) {
+  uint64_t h = 0;
+  if (pos >= 64) {
+    const uint8_t* w = block_src(data, tail, n_main, pos - 64);
+    for (int k = 0; k < 64; k++) h = rotl1_64(h) ^ table[w[k]];
+  } else {
+    for (int k = 0; k < 64; k++) h = rotl1_64(h) ^ table[0];
+  }
+  record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, s_count, s_cand);
+}
+
+#ifndef PFS_EXP_GAHEAD
+#define PFS_EXP_GAHEAD 12
+#endif
+static_assert(PFS_EXP_GAHEAD >= 1 && PFS_EXP_GAHEAD - 1 <= 15, "lgkmcnt is 4 bits");
+constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read_b64 each)
+
+#define PFS_ROLL64G(IN, POS)                                                              \
+  {                                                                                       \
+    uint32_t acc = 0xffffffffu;                                                           \
+    uint64_t ti_[kGAhead];                                                                \
+    StaticFor<0, kGAhead>::run([&](auto tc) {                                             \
+      constexpr int t = decltype(tc)::value;                                              \
+      ti_[t] = lds_read_async(tab_addr(IN[t >> 2], lane_off, t & 3));                     \
+    });                                                                                   \
+    StaticFor<0, 64>::run([&](auto tc) {                                                  \
+      constexpr int t = decltype(tc)::value;                                              \
+      constexpr int inflight = (64 - t < kGAhead) ? 64 - t : kGAhead;                     \
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((inflight - 1) << 8));                         \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      const uint64_t a_ = ti_[t % kGAhead];                                               \
+      PFS_ROT1(nl_, nh_)                                                                  \
+      hl = nl_ ^ (uint32_t)a_;                                                            \
+      hh = nh_ ^ (uint32_t)(a_ >> 32);                                                    \
+      const uint32_t key = (hl ^ ring[t]) & mask32;                                       \
+      ring[t] = hl;                                                                       \
+      acc = acc < key ? acc : key;                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr (t + kGAhead < 64) {                                                   \
+        constexpr int u = t + kGAhead;                                                    \
+        ti_[t % kGAhead] = lds_read_async(tab_addr(IN[u >> 2], lane_off, u & 3));         \
+      }                                                                                   \
+    });                                                                                   \
+    if (__builtin_expect(acc == 0, 0))                                                    \
+      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, s_count,     \
+                     s_cand);                                                             \
+  }
+
 // Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
 // them 128 bytes at a time.  Per step, 8 LDS-DMA instructions (global_load_lds_dwordx4)
 // each fetch one full 128-byte line from 8 strips (8 lines per instruction: the coalesced
@@ -226,7 +287,7 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
 PFS_DEV uint32_t stage_swz(uint32_t r) { return (r >> 1) & 7u; }
 
 template <bool WIDE>
-__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void cdc_scan_kernel(
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs) {
@@ -281,8 +342,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(3, 3
 #pragma unroll
         for (int i = 0; i < 16; i++) prv[i] = 0;  // reset window (writer.go:17-19)
       }
-      // Write(window): h = XOR rotl(T[b_j], 63 - j) == h_{s0-1}
+      // Write(window): h = XOR rotl(T[b_j], 63 - j) == h_{s0-1}.  For the g-form the same
+      // roll from a zero start point gives g over the halo, and its low words seed the ring.
       uint32_t hl = 0, hh = 0;
+      uint32_t ring[64];
 #pragma unroll
       for (int t = 0; t < 64; t++) {
         const uint64_t ti = lds_abs_u64(tab_addr(prv[t >> 2], lane_off, t & 3));
@@ -290,7 +353,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(3, 3
         const uint32_t nh = __builtin_amdgcn_alignbit(hh, hl, 31);
         hl = nl ^ (uint32_t)ti;
         hh = nh ^ (uint32_t)(ti >> 32);
+        ring[t] = hl;
       }
+      const uint32_t mask32 = (uint32_t)mask64;
       const bool active = s0 < n;
       for (uint32_t step = 0; step < kStrip / 128; step++) {
 #ifndef PFS_EXP_NO_DMA_WAIT
@@ -312,11 +377,18 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(3, 3
         if (active && pos < n) {
           uint32_t* c0 = cur;
           uint32_t* c1 = cur + 16;
-          PFS_ROLL64(c0, prv, pos)
-          if (pos + 64 < n) PFS_ROLL64(c1, c0, pos + 64)
+          if constexpr (WIDE) {
+            PFS_ROLL64(c0, prv, pos)
+            if (pos + 64 < n) PFS_ROLL64(c1, c0, pos + 64)
+          } else {
+            PFS_ROLL64G(c0, pos)
+            if (pos + 64 < n) PFS_ROLL64G(c1, pos + 64)
+          }
         }
+        if constexpr (WIDE) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) prv[i] = cur[16 + i];
+          for (int i = 0; i < 16; i++) prv[i] = cur[16 + i];
+        }
       }
     }
     __syncthreads();

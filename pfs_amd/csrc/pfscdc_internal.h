@@ -8,7 +8,7 @@
 namespace pfscdc {
 
 // candidate scan geometry: 512 lanes x 4 KiB strips = 2 MiB tile per workgroup iteration
-constexpr int kScanBlock = 704;  // 11 waves: 64 KiB table + 11 x 8 KiB staging fits 160 KiB
+constexpr int kScanBlock = 512;  // 8 waves (2 per SIMD): 64 KiB table + 8 x 8 KiB staging
 constexpr int kStrip = 4096;
 constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
 constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
