@@ -35,6 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue ceiling: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 integer VOP3 instruction
+# (profiles/r1_ubench_issue_rates.txt: 4.1-4.3 cycles with 2-4 waves per SIMD)
+VALU_PEAK_GIPS = 1024 * 2.4 / 4.0
 GIB = float(1 << 30)
 C4_FILES, C4_FILE_BYTES, C4_TAIL = 10_000, 10_737_418, 2_400
 C3_BYTES = 10 * (1 << 30)
@@ -250,10 +253,19 @@ def main():
         roofline["kernel"] = "blake2b_kernel<true> (ChaCha20 + BLAKE2b of the ciphertext)"
     roofline_cdc = roof(avg["scan"])
     roofline_cdc["kernel"] = "cdc_scan_kernel"
+    rvalu = {}
     if args.traffic_json and os.path.exists(args.traffic_json):
         tj = json.load(open(args.traffic_json))
         roofline["traffic"] = tj.get(roofline["kernel"])
         roofline_cdc["traffic"] = tj.get("cdc_scan_kernel")
+        # the ceiling that binds both kernels: VALU issue (instructions from the PMC pass)
+        for kern, ms in (("blake2b_kernel", avg["hash"]), ("cdc_scan_kernel", avg["scan"])):
+            n = tj.get(kern + "_valu")
+            if n and ms > 0:
+                ach = n / (ms * 1e-3) / 1e9
+                rvalu[kern] = {"bound": "valu-issue", "achieved": round(ach, 1),
+                               "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
+                               "frac": round(ach / VALU_PEAK_GIPS, 4), "valu_per_launch": n}
 
     info.update({"steps_in_flight": S,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
@@ -276,6 +288,8 @@ def main():
         "roofline": roofline,
         "roofline_cdc": roofline_cdc,
     }
+    if rvalu:
+        out["roofline_valu"] = rvalu
 
     if gather and rank == 0 and "index" in last:
         out["dedup"] = hit_rate(last["index"])
