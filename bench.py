@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
                          "§8 next row 1) inside the step")
+    ap.add_argument("--path", default="put", choices=["put", "get"],
+                    help="put: the ingest path (default); get: chunk.Get of the step's chunks "
+                         "(verify BLAKE2b of the stored bytes against Ref.Id, ChaCha20 "
+                         "decrypt), §8 next row 3, device-resident in and out")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="steps in flight (one GPU context + input buffer each)")
@@ -213,6 +217,10 @@ def main():
             kk = (nsteps + k) % S
             if pending[kk]:
                 finish(kk, record)
+
+    if args.path == "get":
+        return bench_get(args, world, rank, local, dev, chunkers[0], batches[0], offs, total,
+                         info, scaling, params, np, torch, dist)
 
     run(args.warmup, False)
     if world > 1:
@@ -377,6 +385,69 @@ def main():
 
     if rank == 0:
         print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    chunker.close()
+
+
+def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, scaling, params,
+              np, torch, dist):
+    """Read path: the step's segments are stored chunks (chunk.Create form); one step =
+    pfscdc_get_chunks over all of them (verify + decrypt, device in/out)."""
+    chunker.set_ref_ids(True)
+    res = chunker.scan(data, offs)  # segments + Ref (id, dek): the chunks as stored
+    segs = res.segments
+    cofs = np.zeros(len(segs) + 1, dtype=np.uint64)
+    cofs[1:] = np.cumsum(segs["size"])  # segments tile the batch in (file, offset) order
+    assert int(cofs[-1]) == total
+    ctext = torch.empty_like(data)
+    _, ok0 = chunker.get_chunks(data, cofs, res.refs, out=ctext)  # XOR is its own inverse
+    assert not ok0.any() or len(segs) == 0  # plaintext never verifies as the stored form
+    out = torch.empty_like(data)
+    for _ in range(args.warmup):
+        chunker.get_chunks(ctext, cofs, res.refs, out=out)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, ok = chunker.get_chunks(ctext, cofs, res.refs, out=out)
+        kms += chunker.last_get_ms()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    same = bool(ok.all()) and bool(torch.equal(out, data))
+    bytes_step = total
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        bytes_step = int(bt.item())
+    K = max(args.steps, 1)
+    ms = kms / K
+    ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    info.update({"path": "get (chunk.Get: verify Ref.Id, ChaCha20 decrypt)",
+                 "chunks_per_step": int(len(segs))})
+    out_line = {
+        "metric": "GiB/s device-resident chunk.Get (verify + decrypt) of stored chunks",
+        "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic plaintext encrypted on the GPU with its own Ref.Dek", "config": info,
+        "kernel_ms": {"get": round(ms, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                     "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
+                     "kernel": "blake2b_kernel<kModeGet>"},
+        "parity": {"all_chunks_verified": bool(ok.all()), "plaintext_equals_original": same},
+    }
+    if rank == 0:
+        print(json.dumps(out_line))
     if world > 1:
         dist.destroy_process_group()
     chunker.close()

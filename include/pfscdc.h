@@ -113,6 +113,18 @@ const pfscdc_ref* pfscdc_refs(const pfscdc_ctx* ctx);
 /* Device time (ms) of the last scan's Ref.Id kernels (0 without PFSCDC_OPT_REF_IDS). */
 int pfscdc_last_ref_ms(pfscdc_ctx* ctx, float* ms);
 
+/* chunk.Get (transform.go:50-78) for a batch of stored chunks, the GetFile read path: for
+ * chunk i (bytes [chunk_offsets[i], chunk_offsets[i+1]) of ctext) compute BLAKE2b-256 of the
+ * stored bytes, set ok[i] = 1 iff it equals refs[i].id (verifyData), and write the ChaCha20
+ * decryption with refs[i].dek to the same range of ptext (CreateOptions{} never compresses).
+ * ctext/ptext: device pointers if *_on_device (16-B aligned ctext), else host memory.
+ * Returns PFSCDC_OK even when some chunk fails verification (see ok[]). */
+int pfscdc_get_chunks(pfscdc_ctx* ctx, const void* ctext, uint64_t nbytes, int ctext_on_device,
+                      const uint64_t* chunk_offsets, uint32_t nchunks, const pfscdc_ref* refs,
+                      void* ptext, int ptext_on_device, uint8_t* ok);
+/* Device time (ms) of the last pfscdc_get_chunks kernels (after the input copy). */
+int pfscdc_last_get_ms(pfscdc_ctx* ctx, float* ms);
+
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
  * positions inside dense tiles are reported through the tile marker instead.  Debug/test
  * hook for the candidate-scan kernel. */

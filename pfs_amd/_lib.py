@@ -31,7 +31,8 @@ EXPORTED = [
     "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
-    "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms",
+    "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms", "pfscdc_get_chunks",
+    "pfscdc_last_get_ms",
     "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
     "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
@@ -140,6 +141,8 @@ def load() -> C.CDLL:
             "pfscdc_set_options": (i32, [vp, u32]),
             "pfscdc_refs": (vp, [vp]),
             "pfscdc_last_ref_ms": (i32, [vp, P(C.c_float)]),
+            "pfscdc_get_chunks": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, i32, vp]),
+            "pfscdc_last_get_ms": (i32, [vp, P(C.c_float)]),
             "pfscdc_host_alloc": (vp, [u64]),
             "pfscdc_host_free": (None, [vp]),
             "pfscdc_fill_synthetic": (i32, [vp, vp, P(u64), u32, u64]),

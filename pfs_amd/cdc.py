@@ -149,6 +149,41 @@ class Chunker:
             t["ref_ids"] = ms.value
         return t
 
+    def get_chunks(self, ctext, chunk_offsets: Sequence[int], refs: np.ndarray, out=None):
+        """chunk.Get for a batch of stored chunks (pfscdc_get_chunks): returns
+        (plaintext, ok[nchunks]).  ``ctext``: host bytes/array or a torch uint8 CUDA tensor;
+        ``out``: optional torch CUDA tensor for device-resident plaintext."""
+        offs = _offsets_array(chunk_offsets)
+        n = len(offs) - 1
+        refs = np.ascontiguousarray(refs, dtype=_lib.ref_dtype())
+        if len(refs) != n:
+            raise ValueError("one ref per chunk")
+        if hasattr(ctext, "is_cuda") and ctext.is_cuda:
+            cptr, nbytes, con = ctext.data_ptr(), ctext.numel(), 1
+        else:
+            arr = np.ascontiguousarray(np.frombuffer(ctext, dtype=np.uint8)
+                                       if isinstance(ctext, (bytes, bytearray)) else ctext,
+                                       dtype=np.uint8)
+            cptr, nbytes, con = (arr.ctypes.data if arr.size else None), arr.size, 0
+            self._get_keep = arr
+        if out is not None:
+            optr, oon, res = out.data_ptr(), 1, out
+        else:
+            res = np.empty(nbytes, dtype=np.uint8)
+            optr, oon = (res.ctypes.data if nbytes else None), 0
+        ok = np.zeros(max(n, 1), dtype=np.uint8)
+        rc = self.lib.pfscdc_get_chunks(self.ctx, cptr, nbytes, con,
+                                        offs.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                                        refs.ctypes.data if n else None, optr, oon,
+                                        ok.ctypes.data)
+        self._check(rc, "get_chunks")
+        return res, ok[:n].astype(bool)
+
+    def last_get_ms(self) -> float:
+        ms = C.c_float()
+        self._check(self.lib.pfscdc_last_get_ms(self.ctx, C.byref(ms)), "get_ms")
+        return ms.value
+
     def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
         out = (C.c_uint64 * cap)()
         n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)

@@ -880,18 +880,23 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
                    : "vcc", "v108", "v109", "v110", "v111");                            \
   } while (0)
 
-// CIPHER = false: DataRef.Hash = BLAKE2b-256(segment) into segs[].hash.
-// CIPHER = true:  Ref.Id = BLAKE2b-256(ChaCha20_dek(segment)) into refs[].id, dek read from
-// refs[].dek (chunk.Create with CreateOptions{}: transform.go:26-46,173-188, client.go:57).
-// The keystream for the two 64-byte ChaCha20 blocks of each 128-byte message block is
-// computed by the same quad (lane j = state column j, DPP diagonals, as for BLAKE2b) and
-// XORed into the LDS message buffer (ds_xor_b32) before the BLAKE2b rounds read it.
-template <bool CIPHER>
+// MODE kModeHash:  DataRef.Hash = BLAKE2b-256(segment) into segs[].hash.
+// MODE kModeRefId: Ref.Id = BLAKE2b-256(ChaCha20_dek(segment)) into refs[].id, dek read from
+//   refs[].dek (chunk.Create with CreateOptions{}: transform.go:26-46,173-188, client.go:57).
+//   The keystream for the two 64-byte ChaCha20 blocks of each 128-byte message block is
+//   computed by the same quad (lane j = state column j, DPP diagonals, as for BLAKE2b) and
+//   XORed into the LDS message buffer (ds_xor_b32) before the BLAKE2b rounds read it.
+// MODE kModeGet:   chunk.Get (transform.go:50-78): the segments are stored chunks; their
+//   BLAKE2b (the id to verify) goes to segs[].hash, and after each block's rounds the
+//   keystream is XORed into the LDS buffer and the plaintext stored to out.
+constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
+template <int MODE>
 __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
-    pfscdc_ref* __restrict__ refs) {
+    pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out) {
+  constexpr bool CIPHER = MODE != kModeHash;
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
   // i&1 while the quad's next block (loaded into registers one iteration earlier) is written
   // to the other buffer halfway through; the wave-uniform parity makes every ds_read offset
@@ -933,6 +938,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   uint64_t ha = 0, hb = 0;
   uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;  // the quad's block blk+1 (lane j: bytes 32j..)
   uint32_t key_b = 0, key_c = 0;  // CIPHER: ChaCha20 key words j and 4+j (state b, c of column j)
+  uint8_t* dst_base = out;         // kModeGet: plaintext of the quad's segment
   const uint32_t cc_a = pick4(j, 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u);
 
   auto lds_put = [&](uint32_t buf) {
@@ -969,6 +975,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
               key_c = dk[4 + j];
             }
             src = data + offs[seg->file] + seg->offset;
+            if (MODE == kModeGet) dst_base = out + offs[seg->file] + seg->offset;
             nblk = L == 0 ? 1 : (L + 127) / 128;
             blk = 0;
             ha = h0a;
@@ -985,7 +992,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
 
     const bool last = blk + 1 == nblk;
-    if (CIPHER) {
+    if (MODE == kModeRefId) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1046,10 +1053,42 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
 #endif
     ha ^= a ^ c;
     hb ^= b ^ d;
+    if (MODE == kModeGet) {  // decrypt the hashed ciphertext block in place, store plaintext
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint32_t ks[4];
+        chacha20_column(ks, cc_a, key_b, key_c, j == 0 ? (uint32_t)(2 * blk + h) : 0u);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_msg + cur + slot + 64 * h) + j;
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+          __hip_atomic_fetch_xor(dst + 4 * w, ks[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int64_t avail = (int64_t)(L - blk * 128) - 32 * (int64_t)j;  // bytes of this lane's piece
+      if (active && avail > 0) {
+        const uint4 p0 = reinterpret_cast<const uint4*>(my + cur)[0];
+        const uint4 p1 = reinterpret_cast<const uint4*>(my + cur)[1];
+        uint8_t* o = dst_base + blk * 128 + 32 * j;
+        if (avail >= 32) {
+          __builtin_memcpy(o, &p0, 16);
+          __builtin_memcpy(o + 16, &p1, 16);
+        } else {
+          uint8_t tmp[32];
+          __builtin_memcpy(tmp, &p0, 16);
+          __builtin_memcpy(tmp + 16, &p1, 16);
+          for (int64_t k = 0; k < avail; k++) o[k] = tmp[k];
+        }
+      }
+    }
     if (active) {
       blk++;
       if (last) {  // digest = h[0..3] little endian; lane j owns h[j]
-        if (CIPHER) reinterpret_cast<uint64_t*>(refs[sidx].id)[j] = ha;
+        if (MODE == kModeRefId) reinterpret_cast<uint64_t*>(refs[sidx].id)[j] = ha;
         else reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
         active = false;
       }
@@ -1383,8 +1422,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
   const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<false><<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order,
-                                                               counter, nbytes, nullptr);
+  blake2b_kernel<kModeHash><<<(unsigned)grid, kHashBlock, 0, st>>>(
+      data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -1398,8 +1437,22 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
   const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<true><<<(unsigned)grid, kHashBlock, 0, st>>>(data, offs, segs, seg_count, order,
-                                                              counter, nbytes, refs);
+  blake2b_kernel<kModeRefId><<<(unsigned)grid, kHashBlock, 0, st>>>(
+      data, offs, segs, seg_count, order, counter, nbytes, refs, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
+                      const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
+                      int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st) {
+  if (nsegs == 0) return hipSuccess;
+  hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
+  const uint64_t quads_per_block = kHashBlock / 4;
+  const uint64_t need = (nsegs + quads_per_block - 1) / quads_per_block;
+  const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
+  const uint64_t grid = need < full ? need : full;
+  blake2b_kernel<kModeGet><<<(unsigned)grid, kHashBlock, 0, st>>>(
+      ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext);
   return hipGetLastError();
 }
 

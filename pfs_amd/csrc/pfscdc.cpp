@@ -79,8 +79,10 @@ struct pfscdc_ctx {
   DevBuf<pfscdc_segment> d_slots, d_segs;
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
   DevBuf<pfscdc_ref> d_refs;
+  DevBuf<uint8_t> d_out;  // get_chunks: plaintext when the caller's output is on the host
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
+  float get_ms = 0.f;
   bool have_refs = false;
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
   PinnedBuf<pfscdc_segment> h_segs;
@@ -219,6 +221,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_qctr.release();
   c->d_refs.release();
   c->h_refs.release();
+  c->d_out.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -418,6 +421,91 @@ int pfscdc_last_timings(pfscdc_ctx* c, float out[5]) {
   HIP_OK(c, hipEventElapsedTime(&out[2], c->ev[2], c->ev[3]));
   HIP_OK(c, hipEventElapsedTime(&out[3], c->ev[3], c->ev[4]));
   HIP_OK(c, hipEventElapsedTime(&out[4], c->ev[0], c->ev[4]));
+  return PFSCDC_OK;
+}
+
+int pfscdc_get_chunks(pfscdc_ctx* c, const void* ctext, uint64_t nbytes, int ctext_on_device,
+                      const uint64_t* chunk_offsets, uint32_t nchunks, const pfscdc_ref* refs,
+                      void* ptext, int ptext_on_device, uint8_t* ok) {
+  if (!c) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "get_chunks during a pending scan");
+  if (!chunk_offsets || (nchunks && (!refs || !ok)) || (nbytes && (!ctext || !ptext)))
+    return fail(c, PFSCDC_EINVAL, "NULL argument");
+  if (chunk_offsets[0] != 0 || chunk_offsets[nchunks] != nbytes)
+    return fail(c, PFSCDC_EINVAL, "chunk_offsets must start at 0 and end at nbytes");
+  for (uint32_t i = 0; i < nchunks; i++)
+    if (chunk_offsets[i + 1] < chunk_offsets[i])
+      return fail(c, PFSCDC_EINVAL, "chunk_offsets must be nondecreasing");
+  if (ctext_on_device && ((uintptr_t)ctext & 15))
+    return fail(c, PFSCDC_EINVAL, "device ctext must be 16-byte aligned");
+  if (nchunks == 0) return PFSCDC_OK;
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  // one segment record per chunk: file i, offset 0 (the kernels address offs[file] + offset)
+  HIP_OK(c, c->h_offs.ensure(nchunks + 1));
+  std::memcpy(c->h_offs.p, chunk_offsets, sizeof(uint64_t) * (nchunks + 1));
+  HIP_OK(c, c->h_segs.ensure(nchunks));
+  for (uint32_t i = 0; i < nchunks; i++) {
+    pfscdc_segment& sg = c->h_segs.p[i];
+    std::memset(&sg, 0, sizeof sg);
+    sg.size = chunk_offsets[i + 1] - chunk_offsets[i];
+    sg.file = i;
+    sg.flags = PFSCDC_SEG_VALID;
+  }
+  HIP_OK(c, c->h_refs.ensure(nchunks));
+  std::memcpy(c->h_refs.p, refs, sizeof(pfscdc_ref) * nchunks);
+  HIP_OK(c, c->d_offs.ensure(nchunks + 1));
+  HIP_OK(c, c->d_segs.ensure(nchunks));
+  HIP_OK(c, c->d_refs.ensure(nchunks));
+  HIP_OK(c, c->d_order.ensure(nchunks));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  HIP_OK(c, c->d_counts.ensure(4));
+  const uint8_t* in;
+  if (ctext_on_device) {
+    in = (const uint8_t*)ctext;
+  } else {
+    HIP_OK(c, c->d_data.ensure(nbytes + 64));
+    HIP_OK(c, hipMemcpyAsync(c->d_data.p, ctext, nbytes, hipMemcpyHostToDevice, st));
+    in = c->d_data.p;
+  }
+  uint8_t* outp;
+  if (ptext_on_device) {
+    outp = (uint8_t*)ptext;
+  } else {
+    HIP_OK(c, c->d_out.ensure(nbytes + 64));
+    outp = c->d_out.p;
+  }
+  HIP_OK(c, c->h_seg_begin.ensure(1));
+  c->h_seg_begin.p[0] = nchunks;  // pinned source for the device segment count
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (nchunks + 1),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * nchunks,
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_refs.p, c->h_refs.p, sizeof(pfscdc_ref) * nchunks,
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipEventRecord(c->ev[7], st));
+  HIP_OK(c, launch_get(in, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, nchunks, c->d_order.p,
+                       c->d_qctr.p, c->num_cus, nbytes, c->d_refs.p, outp, st));
+  HIP_OK(c, hipEventRecord(c->ev[6], st));
+  HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * nchunks,
+                           hipMemcpyDeviceToHost, st));
+  if (!ptext_on_device && nbytes)
+    HIP_OK(c, hipMemcpyAsync(ptext, outp, nbytes, hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  for (uint32_t i = 0; i < nchunks; i++)
+    ok[i] = std::memcmp(c->h_segs.p[i].hash, refs[i].id, 32) == 0 ? 1 : 0;
+  c->nsegs = 0;  // the scan results were overwritten
+  c->have_refs = false;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev[7], c->ev[6]) == hipSuccess) c->get_ms = ms;
+  return PFSCDC_OK;
+}
+
+int pfscdc_last_get_ms(pfscdc_ctx* c, float* ms) {
+  if (!c || !ms) return PFSCDC_EINVAL;
+  *ms = c->get_ms;
   return PFSCDC_OK;
 }
 

@@ -66,3 +66,55 @@ def test_ref_ids_device_resident_batch_and_toggle():
     assert np.array_equal(res.segments, plain.segments)  # refs do not disturb the records
     check_refs(res, t.cpu().numpy(), offs, nmax=24)
     assert c.timings()["ref_ids"] > 0
+
+
+def _encrypt(chunks):
+    """Stored form of each chunk (chunk.Create, CreateOptions{}): ChaCha20_dek(chunk)."""
+    out, refs = [], np.zeros(len(chunks), dtype=[("id", "u1", (32,)), ("dek", "u1", (32,))])
+    for i, ch in enumerate(chunks):
+        rid, dek = Ch.create_ref_id(ch)
+        out.append(Ch.chacha20_xor(dek, ch))
+        refs[i]["id"] = np.frombuffer(rid, dtype=np.uint8)
+        refs[i]["dek"] = np.frombuffer(dek, dtype=np.uint8)
+    return out, refs
+
+
+def test_get_chunks_decrypts_and_verifies():
+    rng = np.random.default_rng(9)
+    lens = [0, 1, 63, 64, 65, 127, 128, 129, 1000, 4096, 70_001, 1 << 20] + \
+        list(rng.integers(1, 300_000, 40))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    plain = synthetic_bytes(offs, 31)
+    chunks = [plain[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+    ctexts, refs = _encrypt(chunks)
+    stored = np.frombuffer(b"".join(ctexts), dtype=np.uint8).copy()
+    c = Chunker(ChunkParams(), 0)
+    pt, ok = c.get_chunks(stored, offs, refs)
+    assert ok.all()
+    assert np.array_equal(pt, plain)
+    # a flipped stored byte fails verification of exactly that chunk (verifyData)
+    bad = stored.copy()
+    k = 7
+    bad[int(offs[k]) + 3] ^= 0x40
+    pt2, ok2 = c.get_chunks(bad, offs, refs)
+    assert not ok2[k] and ok2.sum() == len(lens) - 1
+
+
+def test_get_chunks_device_resident_roundtrip_of_scan_refs():
+    # write path (scan + Ref.Id) then read path (get_chunks) on the same segments
+    import torch
+    offs = (np.arange(9, dtype=np.uint64) * np.uint64(3_000_017))
+    c = Chunker(ChunkParams(), 0, ref_ids=True)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c.fill_synthetic(t, offs, 0xC4)
+    res = c.scan(t, offs)
+    host = t.cpu().numpy()
+    chunks = [host[int(offs[s["file"]]) + int(s["offset"]):][:int(s["size"])].tobytes()
+              for s in res.segments]
+    ctexts = [Ch.chacha20_xor(bytes(r["dek"]), ch) for r, ch in zip(res.refs, chunks)]
+    coffs = np.concatenate([[0], np.cumsum([len(x) for x in chunks])]).astype(np.uint64)
+    dev_ct = torch.from_numpy(np.frombuffer(b"".join(ctexts), dtype=np.uint8).copy()).cuda()
+    out = torch.empty_like(dev_ct)
+    _, ok = c.get_chunks(dev_ct, coffs, res.refs, out=out)
+    assert ok.all()
+    assert np.array_equal(out.cpu().numpy(), np.frombuffer(b"".join(chunks), dtype=np.uint8))
