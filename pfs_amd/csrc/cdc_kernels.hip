@@ -222,8 +222,12 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
 // rotation taken mod 64, h_i = g_i ^ rotl(g_{i-64}, 64) = g_i ^ g_{i-64}: bytes older than the
 // window cancel.  So the scan needs one table lookup per byte (T[in]) instead of two, and
 // the cut test (h_i & mask) == 0 only needs the low word of g_{i-64}: a 64-entry register
-// ring, indexed statically inside the unrolled 64-byte block.  The test itself is one
-// v_bitop3_b32: key = (g_lo ^ ring[t]) & mask.
+// ring, indexed statically inside the unrolled 64-byte block.  The whole recurrence runs in
+// a frame rotated left by kshift = 32 - bits (table entries pre-rotated in LDS; rotation
+// commutes with the XORs), which moves the tested bits to the top of the low word: the
+// key is then just G_lo ^ ring (one v_bitop3_b32 3-way XOR with the new byte's T_lo),
+// min-reduced and compared with 2^kshift, and the new G_lo is written straight into the
+// ring slot it replaces (no copy).
 
 // Rare path for the g-form: rebuild h_{pos-1} from the 64 bytes before pos (zeros before the
 // stream start = the reset window), then re-roll the block exactly like record_block.
@@ -246,6 +250,11 @@ PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __r
 #endif
 static_assert(PFS_EXP_GAHEAD >= 1 && PFS_EXP_GAHEAD - 1 <= 15, "lgkmcnt is 4 bits");
 constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read_b64 each)
+#ifndef PFS_EXP_GWAIT
+#define PFS_EXP_GWAIT 2
+#endif
+constexpr int kGWait = PFS_EXP_GWAIT;  // positions per s_waitcnt
+static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block");
 
 #define PFS_ROLL64G(IN, POS)                                                              \
   {                                                                                       \
@@ -257,15 +266,19 @@ constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read
     });                                                                                   \
     StaticFor<0, 64>::run([&](auto tc) {                                                  \
       constexpr int t = decltype(tc)::value;                                              \
-      constexpr int inflight = (64 - t < kGAhead) ? 64 - t : kGAhead;                     \
-      __builtin_amdgcn_s_waitcnt(0xC07F | ((inflight - 1) << 8));                         \
+      /* one wait per kGWait positions: lookups t .. t+kGWait-1 have landed */             \
+      if constexpr (t % kGWait == 0) {                                                    \
+        constexpr int inflight = (64 - t < kGAhead) ? 64 - t : kGAhead;                   \
+        constexpr int keep = inflight > kGWait ? inflight - kGWait : 0;                   \
+        __builtin_amdgcn_s_waitcnt(0xC07F | (keep << 8));                                 \
+      }                                                                                   \
       __builtin_amdgcn_sched_barrier(0);                                                  \
       const uint64_t a_ = ti_[t % kGAhead];                                               \
       PFS_ROT1(nl_, nh_)                                                                  \
-      hl = nl_ ^ (uint32_t)a_;                                                            \
+      const uint32_t key = xor3(nl_, (uint32_t)a_, ring[t]);                              \
+      ring[t] = nl_ ^ (uint32_t)a_;                                                       \
+      hl = ring[t];                                                                       \
       hh = nh_ ^ (uint32_t)(a_ >> 32);                                                    \
-      const uint32_t key = (hl ^ ring[t]) & mask32;                                       \
-      ring[t] = hl;                                                                       \
       acc = acc < key ? acc : key;                                                        \
       __builtin_amdgcn_sched_barrier(0);                                                  \
       if constexpr (t + kGAhead < 64) {                                                   \
@@ -273,7 +286,7 @@ constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read
         ti_[t % kGAhead] = lds_read_async(tab_addr(IN[u >> 2], lane_off, u & 3));         \
       }                                                                                   \
     });                                                                                   \
-    if (__builtin_expect(acc == 0, 0))                                                    \
+    if (__builtin_expect(acc < cand_thr, 0))                                              \
       record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, s_count,     \
                      s_cand);                                                             \
   }
@@ -301,7 +314,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2
   // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
   for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
     const int idx = i >> 5, c = i & 31;
-    reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] = table[idx];
+    // narrow masks roll in a frame rotated left by kshift = 32 - bits (see PFS_ROLL64G)
+    const uint64_t v = table[idx];
+    reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
+        WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t lane_off = (lane & 31u) * 8u;
@@ -355,7 +371,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2
         hh = nh ^ (uint32_t)(ti >> 32);
         ring[t] = hl;
       }
-      const uint32_t mask32 = (uint32_t)mask64;
+      // rotated frame: the tested low `bits` bits of h sit at the top of the low word, so a
+      // position is a candidate iff (G_lo ^ ring) < 2^kshift, and the block test is a min
+      const uint32_t cand_thr = 1u << kshift;
       const bool active = s0 < n;
       for (uint32_t step = 0; step < kStrip / 128; step++) {
 #ifndef PFS_EXP_NO_DMA_WAIT

@@ -121,6 +121,15 @@ def test_wide_mask():
     assert_same(chunker_for(p).scan(data, offs), data, offs, p)
 
 
+@pytest.mark.parametrize("bits", [1, 2, 9, 16, 31, 32])
+def test_narrow_mask_widths(bits):
+    # the narrow scan rolls in a frame rotated by 32 - bits: every width from 1 to 32
+    p = Ch.Params(average_bits=bits, seed=1, min=100, max=4000)
+    offs = np.array([0, 70_000, 70_001, 200_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 40 + bits)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+
+
 def test_index_writer_seed0_avgbits20():
     # fileset/index/writer.go:60 uses WithRollingHashConfig(20, 0) (then level+1 seeds)
     for seed in (0, 1, 2):
