@@ -125,6 +125,19 @@ int pfscdc_get_chunks(pfscdc_ctx* ctx, const void* ctext, uint64_t nbytes, int c
 /* Device time (ms) of the last pfscdc_get_chunks kernels (after the input copy). */
 int pfscdc_last_get_ms(pfscdc_ctx* ctx, float* ms);
 
+/* chunk.Create(ctx, CreateOptions{}, chunk, createFunc) (transform.go:26-46) for a batch of
+ * formed chunks, the upload half of processChunk (writer.go:233-271): chunk i is bytes
+ * [chunk_offsets[i], chunk_offsets[i+1]) (offsets as for pfscdc_get_chunks).  refs[i] gets
+ * Ref.Dek = Hash(Hash(chunk)) and Ref.Id = Hash(ChaCha20_dek(chunk)).  content_hashes
+ * (NULL or 32 B per chunk) is Hash(chunk) (chunkDataRef.Hash, writer.go:240): taken as
+ * given where hash_known[i] != 0 (e.g. a single-DataRef chunk, whose hash the scan already
+ * has), computed and written back otherwise.  Blocks until refs are on the host. */
+int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
+                       const uint8_t* hash_known, pfscdc_ref* refs);
+/* Device time (ms) of the last chunk.Create batch (pfscdc_create_refs or a writer flush). */
+int pfscdc_last_create_ms(pfscdc_ctx* ctx, float* ms);
+
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
  * positions inside dense tiles are reported through the tile marker instead.  Debug/test
  * hook for the candidate-scan kernel. */
@@ -173,7 +186,8 @@ typedef struct pfscdc_chunk_ref {
   uint64_t chunk_index;  /* 0-based order of createChunk calls */
   int64_t size_bytes;    /* Ref.SizeBytes (== plaintext size: CreateOptions{} => no gzip) */
   int32_t edge;          /* Ref.Edge = first || last (writer.go:200) */
-  int32_t reserved;
+  int32_t has_ref;       /* ref below is set (the writer was created with PFSCDC_OPT_REF_IDS) */
+  pfscdc_ref ref;        /* Ref.Id / Ref.Dek of the whole chunk (maybeUpload, writer.go:255-271) */
 } pfscdc_chunk_ref;
 
 typedef struct pfscdc_annotation_out {
@@ -189,7 +203,10 @@ typedef int (*pfscdc_writer_cb)(void* user, const pfscdc_chunk_ref* chunk,
 
 typedef struct pfscdc_writer pfscdc_writer;
 
-/* batch_bytes: flush threshold for buffered file bytes (0 = 1 GiB). */
+/* batch_bytes: flush threshold for buffered file bytes (0 = 1 GiB).  If ctx has
+ * PFSCDC_OPT_REF_IDS set when the writer is created, every chunk also gets its Ref
+ * (pfscdc_create_refs over the assembled chunk bytes, multi-file chunks and chunks that span
+ * flushes included); the writer's own scans never compute per-segment refs. */
 int pfscdc_writer_create(pfscdc_ctx* ctx, pfscdc_writer_cb cb, void* user,
                          uint64_t batch_bytes, pfscdc_writer** out);
 int pfscdc_writer_annotate(pfscdc_writer* w, uint64_t user);            /* writer.go:118 */
@@ -198,6 +215,21 @@ int pfscdc_writer_close(pfscdc_writer* w);                               /* writ
 int64_t pfscdc_writer_chunk_count(const pfscdc_writer* w);               /* writer.go:113 */
 int64_t pfscdc_writer_annotation_count(const pfscdc_writer* w);          /* writer.go:107 */
 int pfscdc_writer_destroy(pfscdc_writer* w);
+
+/* Chunk formation over a device-resident batch: the chunks chunk.Writer would create
+ * (Annotate cut, CDC cuts, Close's last chunk: writer.go:118-130,198-231,423-438) for the
+ * files of the last pfscdc_scan, each stream k = files [stream_file_begin[k],
+ * stream_file_begin[k+1]) being one writer (one serialized fileset: a fresh chunk.Writer per
+ * fileset.Writer, fileset/writer.go:36-50) that annotates its files in order and closes.
+ * stream_file_begin: nstreams+1 entries from 0 to nfiles (NULL = one stream of all files).
+ * Out: chunk_offsets (cap+1 entries; chunk i = scanned bytes [off[i], off[i+1]), so the
+ * chunks tile the batch), per chunk hash_known/content_hashes as pfscdc_create_refs takes
+ * them (known iff the chunk is one DataRef).  *nchunks = number of chunks; PFSCDC_ENOMEM if
+ * it exceeds cap (outputs truncated).  Must follow the scan directly (PFSCDC_ESTATE after
+ * a pfscdc_create_refs / pfscdc_get_chunks). */
+int pfscdc_form_chunks(pfscdc_ctx* ctx, const uint32_t* stream_file_begin, uint32_t nstreams,
+                       uint64_t* chunk_offsets, uint8_t* content_hashes, uint8_t* hash_known,
+                       uint64_t cap, uint64_t* nchunks);
 
 #ifdef __cplusplus
 }

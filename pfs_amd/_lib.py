@@ -36,6 +36,7 @@ EXPORTED = [
     "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
     "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
+    "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
 ]
 
 
@@ -53,9 +54,13 @@ class DataRef(C.Structure):
     _fields_ = [("hash", C.c_uint8 * 32), ("offset_bytes", C.c_int64), ("size_bytes", C.c_int64)]
 
 
+class RefC(C.Structure):
+    _fields_ = [("id", C.c_uint8 * 32), ("dek", C.c_uint8 * 32)]
+
+
 class ChunkRef(C.Structure):
     _fields_ = [("chunk_index", C.c_uint64), ("size_bytes", C.c_int64), ("edge", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("has_ref", C.c_int32), ("ref", RefC)]
 
 
 class AnnotationOut(C.Structure):
@@ -63,7 +68,7 @@ class AnnotationOut(C.Structure):
                 ("data_ref", DataRef)]
 
 
-assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32
+assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32 and C.sizeof(ChunkRef) == 88
 
 WRITER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(ChunkRef), C.POINTER(AnnotationOut),
                         C.c_uint32)
@@ -154,6 +159,9 @@ def load() -> C.CDLL:
             "pfscdc_writer_chunk_count": (i64, [vp]),
             "pfscdc_writer_annotation_count": (i64, [vp]),
             "pfscdc_writer_destroy": (i32, [vp]),
+            "pfscdc_create_refs": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, vp]),
+            "pfscdc_last_create_ms": (i32, [vp, P(C.c_float)]),
+            "pfscdc_form_chunks": (i32, [vp, P(C.c_uint32), u32, P(u64), vp, vp, u64, P(u64)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

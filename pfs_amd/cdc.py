@@ -179,6 +179,68 @@ class Chunker:
         self._check(rc, "get_chunks")
         return res, ok[:n].astype(bool)
 
+    def form_chunks(self, stream_file_begin: Optional[Sequence[int]] = None):
+        """Chunks chunk.Writer forms over the last scan's files (pfscdc_form_chunks), each
+        stream (files [b[k], b[k+1])) one writer.  Returns (chunk_offsets uint64[n+1],
+        content_hashes uint8[n,32], hash_known bool[n])."""
+        if stream_file_begin is None:
+            sb, ns, sbp = None, 0, None
+        else:
+            sb = np.ascontiguousarray(np.asarray(stream_file_begin, dtype=np.uint32))
+            ns, sbp = len(sb) - 1, sb.ctypes.data_as(C.POINTER(C.c_uint32))
+        cap = max(16, self._nfiles + 16)  # one chunk per 1 MB (min) plus one per stream
+        cap += int(self._offs_keep[-1]) // 1_000_000 if self._nfiles else 0
+        while True:
+            offs = np.zeros(cap + 1, dtype=np.uint64)
+            hashes = np.zeros((cap, 32), dtype=np.uint8)
+            known = np.zeros(cap, dtype=np.uint8)
+            n = C.c_uint64()
+            rc = self.lib.pfscdc_form_chunks(self.ctx, sbp, ns,
+                                             offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                             hashes.ctypes.data, known.ctypes.data, cap,
+                                             C.byref(n))
+            if rc == _lib.PFSCDC_ENOMEM and n.value > cap:
+                cap = n.value
+                continue
+            self._check(rc, "form_chunks")
+            k = n.value
+            return offs[:k + 1].copy(), hashes[:k].copy(), known[:k].astype(bool)
+
+    def create_refs(self, data, chunk_offsets: Sequence[int], content_hashes=None,
+                    hash_known=None):
+        """chunk.Create(CreateOptions{}) per chunk (pfscdc_create_refs).  Returns (refs
+        REF_DTYPE[n], content_hashes uint8[n,32]).  ``data``: host bytes/array or a torch
+        uint8 CUDA tensor."""
+        offs = _offsets_array(chunk_offsets)
+        n = len(offs) - 1
+        hashes = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        known = None
+        if content_hashes is not None:
+            hashes[:n] = np.asarray(content_hashes, dtype=np.uint8).reshape(n, 32)
+            known = np.ascontiguousarray(np.asarray(hash_known, dtype=np.uint8)
+                                         if hash_known is not None else np.ones(n, np.uint8))
+        if hasattr(data, "is_cuda") and data.is_cuda:
+            ptr, nbytes, on = data.data_ptr(), data.numel(), 1
+        else:
+            arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
+                                       if isinstance(data, (bytes, bytearray)) else data,
+                                       dtype=np.uint8)
+            ptr, nbytes, on = (arr.ctypes.data if arr.size else None), arr.size, 0
+            self._create_keep = arr
+        refs = np.zeros(max(n, 1), dtype=_lib.ref_dtype())
+        rc = self.lib.pfscdc_create_refs(self.ctx, ptr, nbytes, on,
+                                         offs.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                                         hashes.ctypes.data,
+                                         known.ctypes.data if known is not None and n else None,
+                                         refs.ctypes.data)
+        self._check(rc, "create_refs")
+        return refs[:n], hashes[:n]
+
+    def last_create_ms(self) -> float:
+        ms = C.c_float()
+        self._check(self.lib.pfscdc_last_create_ms(self.ctx, C.byref(ms)), "create_ms")
+        return ms.value
+
     def last_get_ms(self) -> float:
         ms = C.c_float()
         self._check(self.lib.pfscdc_last_get_ms(self.ctx, C.byref(ms)), "get_ms")

@@ -13,10 +13,13 @@ Reference interface (paths under /root/reference/src/internal/storage/chunk):
 Same names, argument meaning and error behaviour: errors are sticky (writer.go:145-161),
 Write before Annotate is an error (Go panics), callbacks run serially in chunk order
 (chain.go:55-68) and a raised exception inside the callback aborts the writer.
+Every chunk's ``Ref.id``/``Ref.dek`` are those of ``chunk.Create(ctx, CreateOptions{}, ...)``
+(writer.go:255-271, transform.go:26-46), computed on the GPU over the assembled chunk bytes
+(multi-file chunks and chunks spanning flushes included); the upload itself is out of scope.
 Differences: the callback receives fresh ``Annotation`` objects whose ``data`` is the
 annotated object (Go passes the original for the first piece and ``copyAnnotation`` copies
-after a split; both carry the same ``Data``); ``Ref.id`` (the upload object id) is not
-computed on this path yet.
+after a split; both carry the same ``Data``); ``without_ref_ids()`` (no reference
+counterpart) skips the Ref computation for callers that only need DataRef hashes.
 """
 from __future__ import annotations
 
@@ -36,6 +39,7 @@ class Ref:
     edge: bool
     chunk_index: int
     id: bytes = b""
+    dek: bytes = b""
 
 
 @dataclass
@@ -63,6 +67,7 @@ class _WriterConfig:
     min_chunk: int = 1_000_000
     max_chunk: int = 20_000_000
     no_upload: bool = False
+    ref_ids: bool = True
 
 
 def with_rolling_hash_config(average_bits: int, seed: int) -> WriterOption:
@@ -74,6 +79,13 @@ def with_rolling_hash_config(average_bits: int, seed: int) -> WriterOption:
 def with_min_max(min_chunk: int, max_chunk: int) -> WriterOption:
     def opt(c: _WriterConfig) -> None:
         c.min_chunk, c.max_chunk = min_chunk, max_chunk
+    return opt
+
+
+def without_ref_ids() -> WriterOption:
+    """Skip Ref.Id/Dek (not a reference option: the Go writer always runs chunk.Create)."""
+    def opt(c: _WriterConfig) -> None:
+        c.ref_ids = False
     return opt
 
 
@@ -106,7 +118,7 @@ class Writer:
 
         self.lib = _lib.load()
         self._chunker = Chunker(ChunkParams(cfg.average_bits, cfg.seed, cfg.min_chunk,
-                                            cfg.max_chunk), device)
+                                            cfg.max_chunk), device, ref_ids=cfg.ref_ids)
         self._cb = cb
         self._objs: dict[int, object] = {}
         self._next_id = 0
@@ -123,6 +135,8 @@ class Writer:
         try:
             ch = chunk_p.contents
             ref = Ref(size_bytes=ch.size_bytes, edge=bool(ch.edge), chunk_index=ch.chunk_index)
+            if ch.has_ref:
+                ref.id, ref.dek = bytes(ch.ref.id), bytes(ch.ref.dek)
             out = []
             for i in range(n):
                 a = anns_p[i]

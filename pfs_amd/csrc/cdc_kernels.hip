@@ -1445,6 +1445,12 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   return hipGetLastError();
 }
 
+hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
+                        uint32_t* counter, hipStream_t st) {
+  hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
+  return hipGetLastError();
+}
+
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,

@@ -83,7 +83,10 @@ struct pfscdc_ctx {
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
   float get_ms = 0.f;
+  float create_ms = 0.f;
+  std::vector<uint32_t> perm;  // create_refs: record -> chunk
   bool have_refs = false;
+  bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
   PinnedBuf<pfscdc_segment> h_segs;
   hipEvent_t ev[8] = {};
@@ -242,8 +245,12 @@ int pfscdc_set_stream(pfscdc_ctx* c, void* hip_stream) {
   return PFSCDC_OK;
 }
 
-int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
-                      const uint64_t* file_offsets, uint32_t nfiles) {
+}  // extern "C"
+
+namespace {
+
+int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                    const uint64_t* file_offsets, uint32_t nfiles, uint32_t options) {
   if (!c) return PFSCDC_EINVAL;
   if (c->pending) return fail(c, PFSCDC_ESTATE, "previous scan not waited for");
   if (!file_offsets) return fail(c, PFSCDC_EINVAL, "file_offsets is NULL");
@@ -255,6 +262,7 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
       return fail(c, PFSCDC_EINVAL, "file_offsets must be nondecreasing");
   if (bytes_on_device && ((uintptr_t)bytes & 15))
     return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  c->scan_valid = false;
   HIP_OK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
   const pfscdc_params& p = c->params;
@@ -283,7 +291,7 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, c->d_segs.ensure(cap));
   HIP_OK(c, c->d_order.ensure(cap));
   HIP_OK(c, c->d_qctr.ensure(2));
-  if (c->options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
+  if (options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
@@ -332,7 +340,7 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
-  c->have_refs = (c->options & PFSCDC_OPT_REF_IDS) != 0;
+  c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0;
   if (c->have_refs && nfiles)
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, st));
@@ -345,6 +353,16 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
     c->h_seg_begin.p[0] = 0;
   c->pending = true;
   return PFSCDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                      const uint64_t* file_offsets, uint32_t nfiles) {
+  if (!c) return PFSCDC_EINVAL;
+  return scan_async_impl(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles, c->options);
 }
 
 int pfscdc_wait(pfscdc_ctx* c) {
@@ -368,6 +386,7 @@ int pfscdc_wait(pfscdc_ctx* c) {
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->nsegs = total;
+  c->scan_valid = true;
   return PFSCDC_OK;
 }
 
@@ -439,6 +458,7 @@ int pfscdc_get_chunks(pfscdc_ctx* c, const void* ctext, uint64_t nbytes, int cte
   if (ctext_on_device && ((uintptr_t)ctext & 15))
     return fail(c, PFSCDC_EINVAL, "device ctext must be 16-byte aligned");
   if (nchunks == 0) return PFSCDC_OK;
+  c->scan_valid = false;
   HIP_OK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
   // one segment record per chunk: file i, offset 0 (the kernels address offs[file] + offset)
@@ -498,8 +518,43 @@ int pfscdc_get_chunks(pfscdc_ctx* c, const void* ctext, uint64_t nbytes, int cte
     ok[i] = std::memcmp(c->h_segs.p[i].hash, refs[i].id, 32) == 0 ? 1 : 0;
   c->nsegs = 0;  // the scan results were overwritten
   c->have_refs = false;
+  c->scan_valid = false;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, c->ev[7], c->ev[6]) == hipSuccess) c->get_ms = ms;
+  return PFSCDC_OK;
+}
+
+int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
+                       const uint8_t* hash_known, pfscdc_ref* refs) {
+  if (!c) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "create_refs during a pending scan");
+  if (!chunk_offsets || (nchunks && !refs) || (nbytes && !bytes) || (hash_known && !content_hashes))
+    return fail(c, PFSCDC_EINVAL, "NULL argument");
+  if (chunk_offsets[0] != 0 || chunk_offsets[nchunks] != nbytes)
+    return fail(c, PFSCDC_EINVAL, "chunk_offsets must start at 0 and end at nbytes");
+  for (uint32_t i = 0; i < nchunks; i++)
+    if (chunk_offsets[i + 1] < chunk_offsets[i])
+      return fail(c, PFSCDC_EINVAL, "chunk_offsets must be nondecreasing");
+  if (bytes_on_device && ((uintptr_t)bytes & 15))
+    return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  if (nchunks == 0) return PFSCDC_OK;
+  const uint8_t* data;
+  if (bytes_on_device) {
+    data = (const uint8_t*)bytes;
+  } else {
+    HIP_OK(c, hipSetDevice(c->device));
+    HIP_OK(c, c->d_data.ensure(nbytes + 64));
+    HIP_OK(c, hipMemcpyAsync(c->d_data.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
+    data = c->d_data.p;
+  }
+  return create_refs_device(c, data, nbytes, chunk_offsets, nchunks, content_hashes, hash_known,
+                            refs);
+}
+
+int pfscdc_last_create_ms(pfscdc_ctx* c, float* ms) {
+  if (!c || !ms) return PFSCDC_EINVAL;
+  *ms = c->create_ms;
   return PFSCDC_OK;
 }
 
@@ -541,3 +596,94 @@ int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_o
 }
 
 }  // extern "C"
+
+namespace pfscdc {
+
+int ctx_device(const pfscdc_ctx* c) { return c->device; }
+uint32_t ctx_options(const pfscdc_ctx* c) { return c->options; }
+bool ctx_scan_valid(const pfscdc_ctx* c) { return c->scan_valid && !c->pending; }
+uint32_t ctx_nfiles(const pfscdc_ctx* c) { return c->nfiles; }
+uint64_t ctx_file_offset(const pfscdc_ctx* c, uint32_t f) { return c->h_offs.p[f]; }
+
+int scan_sync(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+              const uint64_t* file_offsets, uint32_t nfiles, uint32_t options) {
+  int rc = scan_async_impl(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles, options);
+  if (rc) return rc;
+  return pfscdc_wait(c);
+}
+
+// chunk.Create(ctx, CreateOptions{}, chunk, createFunc) for n chunks of a device buffer
+// (transform.go:26-46): dek = Hash(Hash(chunk)) (deriveKey :173-178), id = Hash(ChaCha20_dek
+// (chunk)) (cryptoXOR :181-188; the id the chunk client stores it under, client.go:57).
+// One record per chunk (file = chunk index, offset 0, over offs).  Chunks whose content hash
+// is not known come first so that one hash pass over records [0, k) computes them; the
+// Ref.Id pass then runs over all n records in its own LPT order.
+int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, const uint64_t* offs,
+                       uint32_t n, uint8_t* hashes, const uint8_t* known, pfscdc_ref* refs) {
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "create_refs during a pending scan");
+  if (n == 0) return PFSCDC_OK;
+  c->scan_valid = false;
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  c->perm.resize(n);
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < n; i++)
+    if (!(known && known[i])) c->perm[k++] = i;
+  for (uint32_t i = 0, r = k; i < n; i++)
+    if (known && known[i]) c->perm[r++] = i;
+  HIP_OK(c, c->h_offs.ensure(n + 1));
+  std::memcpy(c->h_offs.p, offs, sizeof(uint64_t) * (n + 1));
+  HIP_OK(c, c->h_segs.ensure(n));
+  for (uint32_t r = 0; r < n; r++) {
+    const uint32_t i = c->perm[r];
+    pfscdc_segment& sg = c->h_segs.p[r];
+    std::memset(&sg, 0, sizeof sg);
+    sg.size = offs[i + 1] - offs[i];
+    sg.file = i;
+    sg.flags = PFSCDC_SEG_VALID;
+    if (r >= k) std::memcpy(sg.hash, hashes + 32ull * i, 32);
+  }
+  HIP_OK(c, c->d_offs.ensure(n + 1));
+  HIP_OK(c, c->d_segs.ensure(n));
+  HIP_OK(c, c->d_refs.ensure(n));
+  HIP_OK(c, c->d_order.ensure(n));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->h_refs.ensure(n));
+  HIP_OK(c, c->h_seg_begin.ensure(2));
+  c->h_seg_begin.p[0] = k;  // pinned sources of the two device record counts
+  c->h_seg_begin.p[1] = n;
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (n + 1),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * n,
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, 2 * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipEventRecord(c->ev[7], st));
+  if (k)
+    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, k, c->d_order.p,
+                             c->d_qctr.p, c->num_cus, nbytes, st));
+  HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
+  HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
+                           c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, st));
+  HIP_OK(c, hipEventRecord(c->ev[6], st));
+  if (hashes && k)
+    HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * k,
+                             hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, sizeof(pfscdc_ref) * n,
+                           hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  for (uint32_t r = 0; r < n; r++) {
+    const uint32_t i = c->perm[r];
+    refs[i] = c->h_refs.p[r];
+    if (hashes && r < k) std::memcpy(hashes + 32ull * i, c->h_segs.p[r].hash, 32);
+  }
+  c->nsegs = 0;  // the scan results were overwritten
+  c->have_refs = false;
+  c->scan_valid = false;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev[7], c->ev[6]) == hipSuccess) c->create_ms = ms;
+  return PFSCDC_OK;
+}
+
+}  // namespace pfscdc

@@ -46,6 +46,22 @@ void generate_hashes(int64_t seed, uint64_t out[256]);
 const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
 void go_int63(int64_t seed, int64_t* out, int n);
 
+// pfscdc_scan with explicit options (the writer scans without per-segment refs).
+int scan_sync(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+              const uint64_t* file_offsets, uint32_t nfiles, uint32_t options);
+// chunk.Create for chunks i = [offs[i], offs[i+1]) of the device buffer data (nbytes valid
+// bytes; offs absolute, offs[0] may be > 0).  hashes (32 B per chunk, may be NULL): in where
+// known[i], else out (Hash(chunk)).  refs: out.  Synchronous.
+int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
+                       const uint64_t* offs, uint32_t n, uint8_t* hashes, const uint8_t* known,
+                       pfscdc_ref* refs);
+int ctx_device(const pfscdc_ctx* ctx);
+uint32_t ctx_options(const pfscdc_ctx* ctx);
+// the last completed scan: still readable (no create_refs / get_chunks since), its files
+bool ctx_scan_valid(const pfscdc_ctx* ctx);
+uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
+uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
+
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        hipStream_t st);
@@ -62,6 +78,8 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st);
+hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
+                        uint32_t* counter, hipStream_t st);
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,

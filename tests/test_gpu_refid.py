@@ -118,3 +118,62 @@ def test_get_chunks_device_resident_roundtrip_of_scan_refs():
     _, ok = c.get_chunks(dev_ct, coffs, res.refs, out=out)
     assert ok.all()
     assert np.array_equal(out.cpu().numpy(), np.frombuffer(b"".join(chunks), dtype=np.uint8))
+
+
+# ---------------------------------------------------------------- chunk formation + Create
+
+def test_create_refs_matches_oracle_with_known_hashes():
+    rng = np.random.default_rng(21)
+    lens = [0, 1, 64, 127, 128, 129, 5000] + list(rng.integers(1, 400_000, 60))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 41)
+    chunks = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+    c = Chunker(ChunkParams(), 0)
+    refs, hashes = c.create_refs(data, offs)
+    for i, ch in enumerate(chunks):
+        assert bytes(hashes[i]) == Ch.blake2b256(ch)
+        assert (bytes(refs[i]["id"]), bytes(refs[i]["dek"])) == Ch.create_ref_id(ch), i
+    # every other content hash supplied by the caller: same refs, supplied hashes kept
+    known = (np.arange(len(lens)) % 2).astype(np.uint8)
+    given = np.where(known[:, None] == 1, hashes, 0).astype(np.uint8)
+    refs2, hashes2 = c.create_refs(data, offs, given, known)
+    assert np.array_equal(refs2, refs) and np.array_equal(hashes2, hashes)
+
+
+def _oracle_streams(files, p, streams):
+    """Chunks of each stream (one chunk.Writer per stream) with Ref ids, in order."""
+    out = []
+    for b, e in zip(streams[:-1], streams[1:]):
+        if e > b:
+            out.extend(Ch.chunk_stream(files[b:e], p, with_ref_id=True))
+    return out
+
+
+@pytest.mark.parametrize("streams", [None, [0, 17, 17, 60, 95, 120]])
+def test_form_chunks_and_refs_match_writer_streams(streams):
+    import torch
+    p = Ch.Params(average_bits=13, seed=1, min=3000, max=40000)
+    rng = np.random.default_rng(3)
+    lens = [0 if i % 9 == 0 else int(x) for i, x in enumerate(rng.integers(0, 25_000, 120))]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    c = Chunker(ChunkParams(p.average_bits, p.seed, p.min, p.max), 0)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c.fill_synthetic(t, offs, 0x5F)
+    host = t.cpu().numpy()
+    files = [host[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+    c.scan(t, offs)
+    coffs, hashes, known = c.form_chunks(streams)
+    want = _oracle_streams(files, p, streams or [0, len(lens)])
+    assert len(coffs) - 1 == len(want)
+    assert [int(b - a) for a, b in zip(coffs[:-1], coffs[1:])] == [len(ch.data) for ch in want]
+    assert coffs[0] == 0 and coffs[-1] == offs[-1]
+    for i, ch in enumerate(want):
+        assert bytes(host[int(coffs[i]):int(coffs[i + 1])]) == ch.data
+        pieces = [a for a in ch.annotations if a.next_data_ref is not None]
+        assert known[i] == (len(pieces) == 1 and len(ch.data) > 0)
+        if known[i]:
+            assert bytes(hashes[i]) == Ch.blake2b256(ch.data)
+    refs, _ = c.create_refs(t, coffs, hashes, known)
+    for i, ch in enumerate(want):
+        rid, dek = Ch.create_ref_id(ch.data)
+        assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek, i

@@ -1,8 +1,9 @@
 """GPU parity of the chunk.Writer mirror (pfs_amd.chunk over the C ABI writer) against the
 restated reference Writer (oracle.chunker) on whole annotation streams.
 
-Checks every callback: chunk order, Ref.SizeBytes, Ref.Edge, and per annotation the
-NextDataRef {Hash, OffsetBytes, SizeBytes} — including multi-file chunks (the
+Checks every callback: chunk order, Ref.SizeBytes, Ref.Edge, Ref.Id/Dek (chunk.Create with
+CreateOptions{} over the whole chunk, multi-file chunks and chunks spanning writer batches
+included), and per annotation the NextDataRef {Hash, OffsetBytes, SizeBytes} — including multi-file chunks (the
 buf.Len() >= avg cut before a file, writer.go:118-130), size-0 annotations (E2), the empty
 last chunk (E1) and writer batches that split a stream across several GPU scans.
 """
@@ -23,7 +24,8 @@ def run_gpu(files, p: Ch.Params, batch_bytes=1 << 30, writes_per_file=1):
     def cb(anns):
         got.append([(a.data, None if a.next_data_ref is None else
                      (a.next_data_ref.ref.chunk_index, a.next_data_ref.ref.size_bytes,
-                      a.next_data_ref.ref.edge, a.next_data_ref.hash,
+                      a.next_data_ref.ref.edge, a.next_data_ref.ref.id,
+                      a.next_data_ref.ref.dek, a.next_data_ref.hash,
                       a.next_data_ref.offset_bytes, a.next_data_ref.size_bytes)) for a in anns])
 
     w = st.new_writer("chunk-writer", cb, pc.with_rolling_hash_config(p.average_bits, p.seed),
@@ -43,11 +45,12 @@ def run_gpu(files, p: Ch.Params, batch_bytes=1 << 30, writes_per_file=1):
 
 
 def run_oracle(files, p: Ch.Params):
-    chunks = Ch.chunk_stream(files, p, segmenter="numpy")
+    chunks = Ch.chunk_stream(files, p, segmenter="numpy", with_ref_id=True)
     out = []
     for ch in chunks:
         out.append([(a.data, None if a.next_data_ref is None else
-                     (ch.index, len(ch.data), ch.edge, a.next_data_ref.hash,
+                     (ch.index, len(ch.data), ch.edge, a.next_data_ref.ref.id,
+                      a.next_data_ref.ref.dek, a.next_data_ref.hash,
                       a.next_data_ref.offset_bytes, a.next_data_ref.size_bytes))
                     for a in ch.annotations])
     return out, len(chunks)
@@ -93,6 +96,34 @@ def test_writer_stream_ending_on_cut_emits_empty_edge_chunk():
     want, want_n = run_oracle([f], p)
     assert got == want
     assert got[-1] == [(0, None)]             # last chunk is empty, carries no DataRef
+
+
+def test_writer_refs_chunks_spanning_batches():
+    # tiny writer batches: most chunks start in an earlier flush (their bytes are carried)
+    p = Ch.Params(average_bits=14, seed=1, min=3000, max=60000)
+    files = make_files(12, 60, 9_000, zero_every=5)
+    got, nchunks, _ = run_gpu(files, p, batch_bytes=4_000)
+    want, want_n = run_oracle(files, p)
+    assert nchunks == want_n
+    assert got == want
+    ids = {d[3] for ch in got for _, d in ch if d is not None}
+    assert len(ids) == sum(1 for ch in got if any(d is not None for _, d in ch))
+
+
+def test_writer_without_ref_ids_leaves_ref_empty():
+    p = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+    files = make_files(4, 10, 20_000)
+    st = pc.Storage(device=0)
+    refs = []
+    w = st.new_writer("w", lambda anns: refs.extend(a.next_data_ref.ref for a in anns
+                                                     if a.next_data_ref is not None),
+                      pc.with_rolling_hash_config(p.average_bits, p.seed),
+                      pc.with_min_max(p.min, p.max), pc.without_ref_ids())
+    for i, f in enumerate(files):
+        w.annotate(pc.Annotation(data=i))
+        w.write(f)
+    w.close()
+    assert refs and all(r.id == b"" and r.dek == b"" for r in refs)
 
 
 def test_writer_write_before_annotate_is_error():
