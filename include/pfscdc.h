@@ -231,6 +231,67 @@ int pfscdc_form_chunks(pfscdc_ctx* ctx, const uint32_t* stream_file_begin, uint3
                        uint64_t* chunk_offsets, uint8_t* content_hashes, uint8_t* hash_known,
                        uint64_t cap, uint64_t* nchunks);
 
+/* ---- pachd-level stream formation (fileset/unordered_writer.go, fileset/writer.go,
+ * fileset/index/writer.go) --------------------------------------------------------------
+ * An unordered writer buffers Put bytes (host memory) until memThreshold bytes are buffered,
+ * then serializes the buffer as one fileset: files sorted by (path, tag) go through a fresh
+ * chunk writer (pfscdc_writer on data_ctx, Ref ids on), per-file DataRefs are collected by
+ * the fileset.Writer callback, and the additive and deletive index entries go through the
+ * multilevel index writer (level k: its own pfscdc_writer with WithRollingHashConfig(20, k)).
+ * Chunk bytes are not returned (the upload is out of scope); every chunk and every level-0
+ * index entry is reported through the event callback, and each fileset's root indexes are
+ * kept as encoded index.Index protos. */
+
+#define PFSCDC_EV_CHUNK 1 /* a chunk was formed (data or index stream) */
+#define PFSCDC_EV_INDEX 2 /* a level-0 index entry was written (additive or deletive) */
+
+typedef struct pfscdc_uw_event {
+  int32_t kind;           /* PFSCDC_EV_* */
+  int32_t index;          /* -1: the data stream; 0: additive index; 1: deletive index */
+  int32_t level;          /* CHUNK of an index stream: index level */
+  uint32_t fileset;       /* serialized fileset number (UnorderedWriter.subFileSet) */
+  pfscdc_chunk_ref chunk; /* CHUNK: chunk index, size, edge, Ref */
+  const uint8_t* bytes;   /* INDEX: the pbutil frame (int64 LE length + index.Index proto) */
+  uint64_t len;
+} pfscdc_uw_event;
+
+typedef int (*pfscdc_uw_cb)(void* user, const pfscdc_uw_event* ev); /* non-zero aborts */
+
+typedef struct pfscdc_fileset_info {
+  int64_t size_bytes;            /* Primitive.SizeBytes */
+  const uint8_t* additive_root;  /* encoded index.Index (NULL: no additive entries) */
+  uint64_t additive_root_len;
+  const uint8_t* deletive_root;  /* encoded index.Index (NULL: no deletive entries) */
+  uint64_t deletive_root_len;
+  uint32_t num_files;            /* additive entries */
+  uint32_t num_deletes;          /* deletive entries */
+} pfscdc_fileset_info;
+
+typedef struct pfscdc_uwriter pfscdc_uwriter;
+
+/* fileset.Storage.NewUnorderedWriter (fileset/storage.go:84-92).  data_ctx must have
+ * PFSCDC_OPT_REF_IDS set.  mem_threshold: 0 = DefaultMemoryThreshold (1e9 bytes).
+ * index_params: NULL = the reference's index chunking (avgBits 20, seed 0 + level,
+ * 1 MB / 20 MB); other values are a test hook. */
+int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
+                     const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
+                     pfscdc_uwriter** out);
+/* UnorderedWriter.Put(p, tag, appendFile, r) with r = the n bytes at data (tag NULL/"" =
+ * "default"). */
+int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int append_file,
+                  const void* data, uint64_t n);
+/* UnorderedWriter.Delete(p, tag); a path ending in "/" deletes a directory (buffered files
+ * and the live files of the filesets this writer serialized; no parent fileset). */
+int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag);
+int pfscdc_uw_close(pfscdc_uwriter* w); /* serializes the rest (Close, :171-179) */
+uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w);
+/* Fileset i's Primitive (pointers valid until pfscdc_uw_destroy). */
+int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* out);
+int pfscdc_uw_destroy(pfscdc_uwriter* w);
+
+/* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
+int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

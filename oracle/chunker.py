@@ -193,6 +193,7 @@ class Writer:
         ref = Ref(size_bytes=len(chunk), edge=edge, chunk_index=self.chunk_count)
         if self.with_ref_id:
             ref.id, ref.dek = create_ref_id(chunk)
+        self.last_ref = ref
         content_hash = blake2b256(chunk)                     # writer.go:240
         offset = 0
         for a in annotations:                                # writer.go:288-299

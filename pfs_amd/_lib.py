@@ -37,6 +37,8 @@ EXPORTED = [
     "pfscdc_writer_annotate", "pfscdc_writer_write", "pfscdc_writer_close",
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
     "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
+    "pfscdc_uw_create", "pfscdc_uw_put", "pfscdc_uw_delete", "pfscdc_uw_close",
+    "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_path_clean",
 ]
 
 
@@ -67,6 +69,22 @@ class AnnotationOut(C.Structure):
     _fields_ = [("user", C.c_uint64), ("has_data_ref", C.c_int32), ("reserved", C.c_int32),
                 ("data_ref", DataRef)]
 
+
+class UwEvent(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("index", C.c_int32), ("level", C.c_int32),
+                ("fileset", C.c_uint32), ("chunk", ChunkRef), ("bytes", C.c_void_p),
+                ("len", C.c_uint64)]
+
+
+class FilesetInfo(C.Structure):
+    _fields_ = [("size_bytes", C.c_int64), ("additive_root", C.c_void_p),
+                ("additive_root_len", C.c_uint64), ("deletive_root", C.c_void_p),
+                ("deletive_root_len", C.c_uint64), ("num_files", C.c_uint32),
+                ("num_deletes", C.c_uint32)]
+
+
+EV_CHUNK, EV_INDEX = 1, 2
+UW_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(UwEvent))
 
 assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32 and C.sizeof(ChunkRef) == 88
 
@@ -162,6 +180,14 @@ def load() -> C.CDLL:
             "pfscdc_create_refs": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, vp]),
             "pfscdc_last_create_ms": (i32, [vp, P(C.c_float)]),
             "pfscdc_form_chunks": (i32, [vp, P(C.c_uint32), u32, P(u64), vp, vp, u64, P(u64)]),
+            "pfscdc_uw_create": (i32, [vp, i64, P(Params), UW_CB, vp, P(vp)]),
+            "pfscdc_uw_put": (i32, [vp, C.c_char_p, C.c_char_p, i32, vp, u64]),
+            "pfscdc_uw_delete": (i32, [vp, C.c_char_p, C.c_char_p]),
+            "pfscdc_uw_close": (i32, [vp]),
+            "pfscdc_uw_num_filesets": (u32, [vp]),
+            "pfscdc_uw_fileset": (i32, [vp, u32, P(FilesetInfo)]),
+            "pfscdc_uw_destroy": (i32, [vp]),
+            "pfscdc_path_clean": (i32, [C.c_char_p, i32, C.c_char_p, u64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

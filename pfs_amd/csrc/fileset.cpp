@@ -1,0 +1,614 @@
+// fileset.cpp — pachd-level stream formation over the GPU chunk writer (host logic).
+//
+// Reference (paths under /root/reference/src/internal/storage):
+//   fileset/unordered_writer.go:45-179  UnorderedWriter: Put (io.CopyN against memAvailable,
+//                                        serialize at 0), Delete (files; directories over the
+//                                        merged view of what was serialized), Close
+//   fileset/buffer.go:10-106            Buffer (additive/deletive, sorted by path then tag)
+//   fileset/merge.go:37-78,157-164      merged (path, tag) view used by directory deletes
+//   fileset/writer.go:36-182            fileset.Writer: Add, Delete, callback, Close
+//   fileset/index/writer.go:12-162      multilevel index.Writer (level k: avgBits 20, seed k)
+//   fileset/util.go:67-88               Clean / IsDir (Go path.Clean)
+//   pbutil/pbutil.go:64-80              int64 LE length-prefixed protos
+//   chunk/chunk.proto, fileset/index/index.proto, chunk/util.go:25-30 (Reference)
+// Every chunk stream (the data writer of a serialized fileset and each index level) is a
+// pfscdc_writer: CDC, BLAKE2b and chunk.Create run on the GPU; this file is the bookkeeping.
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "pfscdc_internal.h"
+
+namespace {
+
+// ---------------------------------------------------------------- protobuf (proto3) encoder
+
+struct RefT {
+  uint8_t id[32];
+  int64_t size;
+  bool edge;
+  uint8_t dek[32];
+};
+
+struct DataRefT {
+  RefT ref;
+  uint8_t hash[32];
+  int64_t offset, size;
+};
+
+struct IndexT {
+  std::string path;
+  bool has_range = false;
+  int64_t range_offset = 0;
+  std::string range_last_path;
+  RefT range_ref{};
+  std::string tag;  // File is always set on this path (fileset.Writer.Add / Delete)
+  std::vector<DataRefT> data_refs;
+};
+
+void put_varint(std::string& o, uint64_t v) {
+  while (v >= 0x80) {
+    o.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)v);
+}
+void put_key(std::string& o, int field, int wire) { put_varint(o, (uint64_t)(field << 3 | wire)); }
+void put_bytes(std::string& o, int field, const void* p, size_t n) {
+  if (!n) return;  // proto3: empty bytes/strings are not emitted
+  put_key(o, field, 2);
+  put_varint(o, n);
+  o.append((const char*)p, n);
+}
+void put_int(std::string& o, int field, int64_t v) {
+  if (!v) return;
+  put_key(o, field, 0);
+  put_varint(o, (uint64_t)v);
+}
+void put_msg(std::string& o, int field, const std::string& m) {  // set messages: always emitted
+  put_key(o, field, 2);
+  put_varint(o, m.size());
+  o += m;
+}
+
+// chunk.Ref as chunk.Create + processChunk leave it: EncryptionAlgo CHACHA20 (1),
+// CompressionAlgo NONE (0, not emitted)
+std::string enc_ref(const RefT& r) {
+  std::string o;
+  put_bytes(o, 1, r.id, 32);
+  put_int(o, 2, r.size);
+  put_int(o, 3, r.edge ? 1 : 0);
+  put_bytes(o, 4, r.dek, 32);
+  put_int(o, 5, 1);
+  return o;
+}
+
+std::string enc_dataref(const RefT& r, const uint8_t* hash, int64_t offset, int64_t size) {
+  std::string o;
+  put_msg(o, 1, enc_ref(r));
+  if (hash) put_bytes(o, 2, hash, 32);
+  put_int(o, 3, offset);
+  put_int(o, 4, size);
+  return o;
+}
+
+std::string enc_index(const IndexT& x) {
+  std::string o;
+  put_bytes(o, 1, x.path.data(), x.path.size());
+  if (x.has_range) {
+    std::string r;
+    put_int(r, 1, x.range_offset);
+    put_bytes(r, 2, x.range_last_path.data(), x.range_last_path.size());
+    // chunk.Reference(dataRef) = {Ref, SizeBytes: Ref.SizeBytes}
+    put_msg(r, 3, enc_dataref(x.range_ref, nullptr, 0, x.range_ref.size));
+    put_msg(o, 2, r);
+  }
+  std::string f;
+  put_bytes(f, 1, x.tag.data(), x.tag.size());
+  for (const DataRefT& d : x.data_refs) put_msg(f, 2, enc_dataref(d.ref, d.hash, d.offset, d.size));
+  put_msg(o, 3, f);
+  return o;
+}
+
+std::string frame(const std::string& m) {  // pbutil WriteBytes
+  std::string o(8, '\0');
+  const uint64_t n = m.size();
+  for (int i = 0; i < 8; i++) o[i] = (char)(n >> (8 * i));
+  return o + m;
+}
+
+RefT ref_of(const pfscdc_chunk_ref* c) {
+  RefT r{};
+  std::memcpy(r.id, c->ref.id, 32);
+  std::memcpy(r.dek, c->ref.dek, 32);
+  r.size = c->size_bytes;
+  r.edge = c->edge != 0;
+  return r;
+}
+
+// ---------------------------------------------------------------- paths (Go path.Clean)
+
+std::string go_path_clean(const std::string& p) {
+  if (p.empty()) return ".";
+  const bool rooted = p[0] == '/';
+  const size_t n = p.size();
+  std::string out;
+  size_t r = 0, dotdot = 0;
+  if (rooted) {
+    out.push_back('/');
+    r = dotdot = 1;
+  }
+  while (r < n) {
+    if (p[r] == '/') {
+      r++;
+    } else if (p[r] == '.' && (r + 1 == n || p[r + 1] == '/')) {
+      r++;
+    } else if (p[r] == '.' && r + 1 < n && p[r + 1] == '.' && (r + 2 == n || p[r + 2] == '/')) {
+      r += 2;
+      if (out.size() > dotdot) {
+        size_t w = out.size() - 1;
+        while (w > dotdot && out[w] != '/') w--;
+        out.resize(w);
+      } else if (!rooted) {
+        if (!out.empty()) out.push_back('/');
+        out += "..";
+        dotdot = out.size();
+      }
+    } else {
+      if ((rooted && out.size() != 1) || (!rooted && !out.empty())) out.push_back('/');
+      for (; r < n && p[r] != '/'; r++) out.push_back(p[r]);
+    }
+  }
+  return out.empty() ? "." : out;
+}
+
+bool is_dir(const std::string& p) { return !p.empty() && p.back() == '/'; }
+
+std::string clean(const std::string& p0, bool dir) {  // fileset/util.go:67-77
+  std::string p = go_path_clean(p0);
+  if (p == ".") return "/";
+  size_t a = 0, b = p.size();
+  while (a < b && p[a] == '/') a++;
+  while (b > a && p[b - 1] == '/') b--;
+  std::string y = "/" + p.substr(a, b - a);
+  if (dir && !is_dir(y)) y += "/";
+  return y;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- writers
+
+struct pfscdc_uwriter;
+
+namespace {
+
+struct Streams {  // the ctxs of every chunk stream kind; events out
+  pfscdc_ctx* data_ctx = nullptr;
+  pfscdc_params index_params{};
+  std::map<int64_t, pfscdc_ctx*> index_ctx;  // by seed (= level)
+  pfscdc_uw_cb cb = nullptr;
+  void* user = nullptr;
+  uint32_t fileset = 0;
+  int err = 0;
+
+  int emit(pfscdc_uw_event& ev) {
+    ev.fileset = fileset;
+    if (cb && cb(user, &ev) != 0) return PFSCDC_ECALLBACK;
+    return PFSCDC_OK;
+  }
+  pfscdc_ctx* level_ctx(int level) {
+    auto it = index_ctx.find(level);
+    if (it != index_ctx.end()) return it->second;
+    pfscdc_params p = index_params;
+    p.seed = index_params.seed + level;
+    pfscdc_ctx* c = nullptr;
+    if (pfscdc_ctx_create(&p, pfscdc::ctx_device(data_ctx), &c) != PFSCDC_OK) return nullptr;
+    pfscdc_set_options(c, PFSCDC_OPT_REF_IDS);
+    index_ctx[level] = c;
+    return c;
+  }
+  ~Streams() {
+    for (auto& kv : index_ctx) pfscdc_ctx_destroy(kv.second);
+  }
+};
+
+struct IndexWriter;
+constexpr int kMaxIndexLevels = 32;
+
+struct Level {
+  IndexWriter* iw;
+  int level;
+  pfscdc_writer* cw = nullptr;
+  IndexT* last = nullptr;
+};
+
+struct IndexWriter {  // index/writer.go:27-162
+  Streams* st;
+  int which;  // 0 additive, 1 deletive
+  std::vector<std::unique_ptr<Level>> levels;
+  bool closed = false;
+  IndexT* root = nullptr;
+  std::vector<std::unique_ptr<IndexT>>* pool;
+
+  ~IndexWriter() {
+    for (auto& l : levels)
+      if (l->cw) pfscdc_writer_destroy(l->cw);
+  }
+
+  int new_level() {
+    const int k = (int)levels.size();
+    pfscdc_ctx* c = st->level_ctx(k);
+    if (!c) return PFSCDC_EHIP;
+    auto l = std::make_unique<Level>();
+    l->iw = this;
+    l->level = k;
+    int rc = pfscdc_writer_create(c, &IndexWriter::callback, l.get(), 0, &l->cw);
+    if (rc) return rc;
+    levels.push_back(std::move(l));
+    return PFSCDC_OK;
+  }
+
+  int write_index(IndexT* idx, int level) {
+    if (levels.empty()) {
+      int rc = new_level();
+      if (rc) return rc;
+    }
+    const std::string b = frame(enc_index(*idx));
+    if (level == 0) {
+      pfscdc_uw_event ev{};
+      ev.kind = PFSCDC_EV_INDEX;
+      ev.index = which;
+      ev.bytes = (const uint8_t*)b.data();
+      ev.len = b.size();
+      int rc = st->emit(ev);
+      if (rc) return rc;
+    }
+    pfscdc_writer* cw = levels[level]->cw;
+    int rc = pfscdc_writer_annotate(cw, (uint64_t)(uintptr_t)idx);
+    if (!rc) rc = pfscdc_writer_write(cw, b.data(), b.size());
+    return rc;
+  }
+
+  static int callback(void* user, const pfscdc_chunk_ref* chunk, const pfscdc_annotation_out* a,
+                      uint32_t n) {
+    Level* lw = (Level*)user;
+    IndexWriter* w = lw->iw;
+    pfscdc_uw_event ev{};
+    ev.kind = PFSCDC_EV_CHUNK;
+    ev.index = w->which;
+    ev.level = lw->level;
+    ev.chunk = *chunk;
+    int rc = w->st->emit(ev);
+    if (rc || n == 0) return rc;
+    IndexT* idx = (IndexT*)(uintptr_t)a[0].user;
+    const pfscdc_annotation_out* dr = &a[0];
+    if (n > 1 && lw->last && idx->path == lw->last->path) {  // started in the previous chunk
+      idx = (IndexT*)(uintptr_t)a[1].user;
+      dr = &a[1];
+    }
+    lw->last = (IndexT*)(uintptr_t)a[n - 1].user;
+    const std::string last_path = lw->last->has_range ? lw->last->range_last_path : lw->last->path;
+    if (!dr->has_data_ref) return PFSCDC_ESTATE;  // Go dereferences a nil NextDataRef here
+    idx->has_range = true;
+    idx->range_offset = dr->data_ref.offset_bytes;
+    idx->range_last_path = last_path;
+    idx->range_ref = ref_of(chunk);
+    if (w->closed) w->root = idx;
+    const int level = lw->level;  // lw stays valid: levels hold unique_ptrs
+    if (level == (int)w->levels.size() - 1) {
+      // an entry >= the index avg is cut before at every level and the levels never
+      // converge (Go keeps adding levels); the reference's 1 MiB avg rules that out
+      if (level + 1 >= kMaxIndexLevels) return PFSCDC_EUNSUPPORTED;
+      rc = w->new_level();
+      if (rc) return rc;
+    }
+    return w->write_index(idx, level + 1);
+  }
+
+  int close(IndexT** out) {
+    closed = true;
+    for (size_t i = 0; i < levels.size(); i++) {
+      pfscdc_writer* cw = levels[i]->cw;
+      int rc = pfscdc_writer_close(cw);
+      if (rc) return rc;
+      if (pfscdc_writer_annotation_count(cw) == 1 && pfscdc_writer_chunk_count(cw) == 1) break;
+    }
+    *out = root;
+    return PFSCDC_OK;
+  }
+};
+
+struct FilesetInfo {
+  int64_t size_bytes = 0;
+  std::string additive, deletive;  // encoded root Index
+  bool has_additive = false, has_deletive = false;
+  std::vector<std::pair<std::string, std::string>> files, deletes;  // (path, tag) in order
+};
+
+struct FilesetWriter {  // fileset/writer.go:21-182
+  Streams* st;
+  std::vector<std::unique_ptr<IndexT>> pool;
+  IndexWriter additive, deletive;
+  pfscdc_writer* cw = nullptr;
+  IndexT *idx = nullptr, *delete_idx = nullptr, *last_idx = nullptr;
+  FilesetInfo info;
+  int err = 0;
+
+  explicit FilesetWriter(Streams* s) : st(s), additive{s, 0, {}, false, nullptr, &pool},
+                                       deletive{s, 1, {}, false, nullptr, &pool} {}
+  ~FilesetWriter() {
+    if (cw) pfscdc_writer_destroy(cw);
+  }
+
+  int open() { return pfscdc_writer_create(st->data_ctx, &FilesetWriter::callback, this, 0, &cw); }
+
+  static int check_path(const IndexT* prev, const IndexT* idx) {
+    if (!prev) return PFSCDC_OK;
+    if (prev->path == idx->path && prev->tag == idx->tag) return PFSCDC_EINVAL;  // same path twice
+    if (prev->path > idx->path) return PFSCDC_EINVAL;                            // out of order
+    return PFSCDC_OK;
+  }
+
+  IndexT* make(const std::string& path, const std::string& tag) {
+    pool.push_back(std::make_unique<IndexT>());
+    pool.back()->path = path;
+    pool.back()->tag = tag;
+    return pool.back().get();
+  }
+
+  int add(const std::string& path, const std::string& tag, const std::string& data) {
+    IndexT* x = make(path, tag);
+    int rc = check_path(idx, x);
+    if (rc) return rc;
+    idx = x;
+    info.files.emplace_back(path, tag);
+    rc = pfscdc_writer_annotate(cw, (uint64_t)(uintptr_t)x);
+    if (!rc) rc = pfscdc_writer_write(cw, data.data(), data.size());
+    info.size_bytes += (int64_t)data.size();
+    return rc;
+  }
+
+  int del(const std::string& path, const std::string& tag) {
+    IndexT* x = make(path, tag);
+    int rc = check_path(delete_idx, x);
+    if (rc) return rc;
+    delete_idx = x;
+    info.deletes.emplace_back(path, tag);
+    return deletive.write_index(x, 0);
+  }
+
+  static int callback(void* user, const pfscdc_chunk_ref* chunk, const pfscdc_annotation_out* a,
+                      uint32_t n) {
+    FilesetWriter* w = (FilesetWriter*)user;
+    pfscdc_uw_event ev{};
+    ev.kind = PFSCDC_EV_CHUNK;
+    ev.index = -1;
+    ev.chunk = *chunk;
+    int rc = w->st->emit(ev);
+    if (rc) return rc;
+    const RefT ref = ref_of(chunk);
+    for (uint32_t i = 0; i < n; i++) {
+      IndexT* x = (IndexT*)(uintptr_t)a[i].user;
+      if (!w->last_idx) w->last_idx = x;
+      if (x->path != w->last_idx->path || x->tag != w->last_idx->tag) {
+        rc = w->additive.write_index(w->last_idx, 0);
+        if (rc) return rc;
+        w->last_idx = x;
+      }
+      if (a[i].has_data_ref) {
+        DataRefT d{};
+        d.ref = ref;
+        std::memcpy(d.hash, a[i].data_ref.hash, 32);
+        d.offset = a[i].data_ref.offset_bytes;
+        d.size = a[i].data_ref.size_bytes;
+        w->last_idx->data_refs.push_back(d);
+      }
+    }
+    return PFSCDC_OK;
+  }
+
+  int close() {
+    int rc = pfscdc_writer_close(cw);
+    if (rc) return rc;
+    if (last_idx) {
+      rc = additive.write_index(last_idx, 0);
+      if (rc) return rc;
+    }
+    IndexT *a = nullptr, *d = nullptr;
+    rc = additive.close(&a);
+    if (!rc) rc = deletive.close(&d);
+    if (rc) return rc;
+    if (a) {
+      info.has_additive = true;
+      info.additive = enc_index(*a);
+    }
+    if (d) {
+      info.has_deletive = true;
+      info.deletive = enc_index(*d);
+    }
+    return PFSCDC_OK;
+  }
+};
+
+struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFiles does
+  std::map<std::string, std::map<std::string, std::string>> additive;
+  std::map<std::string, std::set<std::string>> deletive;
+
+  std::string& add(const std::string& path0, const std::string& tag) {
+    return additive[clean(path0, false)][tag];
+  }
+  void del(const std::string& path0, const std::string& tag) {
+    const std::string path = clean(path0, is_dir(path0));
+    if (is_dir(path)) {
+      for (auto it = additive.lower_bound(path); it != additive.end() &&
+                                                 it->first.compare(0, path.size(), path) == 0;)
+        it = additive.erase(it);
+      return;
+    }
+    auto it = additive.find(path);
+    if (it != additive.end()) it->second.erase(tag);  // the (now maybe empty) path entry stays
+    deletive[path].insert(tag);
+  }
+  bool empty() const { return additive.empty() && deletive.empty(); }
+};
+
+}  // namespace
+
+struct pfscdc_uwriter {  // unordered_writer.go:15-26
+  Streams st;
+  int64_t mem_threshold = 1000000000;
+  int64_t mem_available = 1000000000;
+  Buffer buffer;
+  std::vector<FilesetInfo> filesets;
+  bool closed = false;
+  int err = 0;
+
+  int fail(int rc) {
+    if (!err) err = rc;
+    return err;
+  }
+
+  int serialize() {  // unordered_writer.go:83-122
+    if (buffer.empty()) return PFSCDC_OK;
+    FilesetWriter fw(&st);
+    int rc = fw.open();
+    for (auto& p : buffer.additive)
+      for (auto& t : p.second)
+        if (!rc) rc = fw.add(p.first, t.first, t.second);
+    for (auto& p : buffer.deletive)
+      for (auto& t : p.second)
+        if (!rc) rc = fw.del(p.first, t);
+    if (!rc) rc = fw.close();
+    if (rc) return rc;
+    filesets.push_back(std::move(fw.info));
+    buffer = Buffer();
+    mem_available = mem_threshold;
+    st.fileset++;
+    return PFSCDC_OK;
+  }
+
+  int put(const std::string& p, std::string tag, bool append, const uint8_t* data, uint64_t n) {
+    if (tag.empty()) tag = "default";
+    if (!append) buffer.del(p, tag);
+    std::string* w = &buffer.add(p, tag);
+    uint64_t pos = 0;
+    for (;;) {  // io.CopyN(w, r, memAvailable): EOF iff fewer than memAvailable bytes were left
+      const uint64_t want = (uint64_t)mem_available;
+      const uint64_t got = std::min<uint64_t>(want, n - pos);
+      w->append((const char*)data + pos, got);
+      pos += got;
+      mem_available -= (int64_t)got;
+      if (got < want) return PFSCDC_OK;
+      if (mem_available == 0) {
+        int rc = serialize();
+        if (rc) return rc;
+        w = &buffer.add(p, tag);
+      }
+    }
+  }
+
+  int del(const std::string& p0, std::string tag) {  // unordered_writer.go:125-149
+    if (tag.empty()) tag = "default";
+    const std::string p = clean(p0, is_dir(p0));
+    if (!is_dir(p)) {
+      buffer.del(p, tag);
+      return PFSCDC_OK;
+    }
+    buffer.del(p, tag);
+    // merged view of the serialized filesets (merge.go: a (path, tag) group is live iff its
+    // last stream, deletive before additive within a fileset, is additive)
+    std::map<std::pair<std::string, std::string>, bool> live;
+    for (const FilesetInfo& fs : filesets) {
+      for (auto& k : fs.deletes) live[k] = false;
+      for (auto& k : fs.files) live[k] = true;
+    }
+    for (auto& kv : live)
+      if (kv.second && kv.first.first.compare(0, p.size(), p) == 0) buffer.del(kv.first.first, tag);
+    return PFSCDC_OK;
+  }
+};
+
+extern "C" {
+
+int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
+                     const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
+                     pfscdc_uwriter** out) {
+  if (!data_ctx || !out || mem_threshold < 0) return PFSCDC_EINVAL;
+  if (!(pfscdc::ctx_options(data_ctx) & PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
+  pfscdc_uwriter* w = new pfscdc_uwriter();
+  w->st.data_ctx = data_ctx;
+  w->st.cb = cb;
+  w->st.user = user;
+  if (index_params) {
+    w->st.index_params = *index_params;
+  } else {  // index/writer.go:13,60: WithRollingHashConfig(20, level), default min/max
+    pfscdc_default_params(&w->st.index_params);
+    w->st.index_params.average_bits = 20;
+    w->st.index_params.seed = 0;
+  }
+  if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
+  *out = w;
+  return PFSCDC_OK;
+}
+
+int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int append_file,
+                  const void* data, uint64_t n) {
+  if (!w || !path || (n && !data)) return PFSCDC_EINVAL;
+  if (w->err) return w->err;
+  if (w->closed) return w->fail(PFSCDC_ESTATE);
+  int rc = w->put(path, tag ? tag : "", append_file != 0, (const uint8_t*)data, n);
+  return rc ? w->fail(rc) : PFSCDC_OK;
+}
+
+int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag) {
+  if (!w || !path) return PFSCDC_EINVAL;
+  if (w->err) return w->err;
+  if (w->closed) return w->fail(PFSCDC_ESTATE);
+  int rc = w->del(path, tag ? tag : "");
+  return rc ? w->fail(rc) : PFSCDC_OK;
+}
+
+int pfscdc_uw_close(pfscdc_uwriter* w) {
+  if (!w) return PFSCDC_EINVAL;
+  if (w->err) return w->err;
+  if (w->closed) return PFSCDC_OK;
+  w->closed = true;
+  int rc = w->serialize();
+  return rc ? w->fail(rc) : PFSCDC_OK;
+}
+
+uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w) {
+  return w ? (uint32_t)w->filesets.size() : 0;
+}
+
+int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* out) {
+  if (!w || !out || i >= w->filesets.size()) return PFSCDC_EINVAL;
+  const FilesetInfo& f = w->filesets[i];
+  out->size_bytes = f.size_bytes;
+  out->additive_root = f.has_additive ? (const uint8_t*)f.additive.data() : nullptr;
+  out->additive_root_len = f.has_additive ? f.additive.size() : 0;
+  out->deletive_root = f.has_deletive ? (const uint8_t*)f.deletive.data() : nullptr;
+  out->deletive_root_len = f.has_deletive ? f.deletive.size() : 0;
+  out->num_files = (uint32_t)f.files.size();
+  out->num_deletes = (uint32_t)f.deletes.size();
+  return PFSCDC_OK;
+}
+
+int pfscdc_uw_destroy(pfscdc_uwriter* w) {
+  delete w;
+  return PFSCDC_OK;
+}
+
+int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap) {
+  if (!path || !out) return PFSCDC_EINVAL;
+  const std::string y = clean(path, is_directory != 0);
+  if (y.size() + 1 > cap) return PFSCDC_ENOMEM;
+  std::memcpy(out, y.c_str(), y.size() + 1);
+  return PFSCDC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+"""Host-side mirror of the reference's pachd write path above chunk.Writer, over the C ABI.
+
+Reference interface (paths under /root/reference/src/internal/storage/fileset):
+
+* ``Storage.NewUnorderedWriter(ctx, ...)``                         storage.go:84-92
+* ``UnorderedWriter.Put(p, tag, appendFile, r) / Delete(p, tag) / Close()``
+                                                                   unordered_writer.go:45-179
+* ``fileset.Writer`` (Add / Delete / callback / Close) and the multilevel ``index.Writer``
+  run inside the library per serialized fileset (writer.go:36-182, index/writer.go:27-162)
+* ``Clean(p, isDir)``                                              util.go:67-77
+
+Same names, argument meaning and error behaviour (errors are sticky; an out-of-order or
+duplicate path inside a fileset is an error).  ``close()`` returns one ``Primitive`` per
+serialized fileset (SizeBytes and the encoded root ``index.Index`` of the additive and
+deletive indexes); the fileset ids and the composite of the Postgres metadata store, and the
+chunk upload, are out of scope.  ``events`` records, per fileset, every formed chunk (data and
+index streams, with its Ref.Id) and every level-0 index entry (pbutil frame).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+from . import _lib
+from .cdc import ChunkParams, Chunker
+
+DEFAULT_FILE_TAG = "default"
+DEFAULT_MEMORY_THRESHOLD = 10 ** 9
+
+
+@dataclass
+class Primitive:
+    additive: Optional[bytes]
+    deletive: Optional[bytes]
+    size_bytes: int
+    num_files: int
+    num_deletes: int
+
+
+def clean(p: str, is_dir: bool) -> str:
+    out = C.create_string_buffer(len(p.encode()) + 4)
+    rc = _lib.load().pfscdc_path_clean(p.encode(), int(is_dir), out, len(out))
+    if rc:
+        raise _lib.PfsCdcError(rc, "path_clean")
+    return out.value.decode()
+
+
+class Storage:
+    """``fileset.Storage`` restricted to the write path, bound to one GPU."""
+
+    def __init__(self, device: int = 0, params: ChunkParams = ChunkParams(),
+                 mem_threshold: int = DEFAULT_MEMORY_THRESHOLD,
+                 index_params: Optional[ChunkParams] = None):
+        self.device, self.params = device, params
+        self.mem_threshold, self.index_params = mem_threshold, index_params
+
+    def new_unordered_writer(self) -> "UnorderedWriter":
+        return UnorderedWriter(self)
+
+
+class UnorderedWriter:
+    def __init__(self, storage: Storage):
+        self.lib = _lib.load()
+        self._chunker = Chunker(storage.params, storage.device, ref_ids=True)
+        self.events: list = []
+        self._exc: Optional[BaseException] = None
+        self._cfun = _lib.UW_CB(self._on_event)
+        ip = storage.index_params.to_c() if storage.index_params else None
+        w = C.c_void_p()
+        rc = self.lib.pfscdc_uw_create(self._chunker.ctx, storage.mem_threshold,
+                                       C.byref(ip) if ip is not None else None, self._cfun, None,
+                                       C.byref(w))
+        if rc:
+            raise _lib.PfsCdcError(rc, "pfscdc_uw_create")
+        self._w = w
+
+    def _on_event(self, _user, ev_p) -> int:
+        try:
+            ev = ev_p.contents
+            while len(self.events) <= ev.fileset:
+                self.events.append([])
+            if ev.kind == _lib.EV_CHUNK:
+                ch = ev.chunk
+                self.events[ev.fileset].append(
+                    ("chunk", ev.index, ev.level if ev.index >= 0 else 0, ch.size_bytes,
+                     bool(ch.edge), bytes(ch.ref.id)))
+            else:
+                self.events[ev.fileset].append(("index", ev.index, C.string_at(ev.bytes, ev.len)))
+            return 0
+        except BaseException as e:
+            self._exc = e
+            return 1
+
+    def _check(self, rc: int, what: str) -> None:
+        if self._exc is not None:
+            exc, self._exc = self._exc, None
+            raise exc
+        if rc:
+            msg = self.lib.pfscdc_last_error(self._chunker.ctx)
+            raise _lib.PfsCdcError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def put(self, p: str, tag: str, append_file: bool, data) -> None:
+        buf = bytes(data)
+        self._check(self.lib.pfscdc_uw_put(self._w, p.encode(), tag.encode(), int(append_file),
+                                           buf, len(buf)), "Put")
+
+    def delete(self, p: str, tag: str = "") -> None:
+        self._check(self.lib.pfscdc_uw_delete(self._w, p.encode(), tag.encode()), "Delete")
+
+    def close(self) -> list:
+        self._check(self.lib.pfscdc_uw_close(self._w), "Close")
+        out = []
+        for i in range(self.lib.pfscdc_uw_num_filesets(self._w)):
+            info = _lib.FilesetInfo()
+            self._check(self.lib.pfscdc_uw_fileset(self._w, i, C.byref(info)), "fileset")
+            a = C.string_at(info.additive_root, info.additive_root_len) if info.additive_root else None
+            d = C.string_at(info.deletive_root, info.deletive_root_len) if info.deletive_root else None
+            out.append(Primitive(a, d, info.size_bytes, info.num_files, info.num_deletes))
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "_w", None):
+                self.lib.pfscdc_uw_destroy(self._w)
+                self._w = None
+            if getattr(self, "_chunker", None):
+                self._chunker.close()
+        except Exception:
+            pass

@@ -1,0 +1,127 @@
+"""GPU parity of pachd-level stream formation (§8(f) rows 2-3): UnorderedWriter -> fileset.Writer
+-> chunk.Writer (GPU) -> multilevel index.Writer, against the restated reference
+(oracle/fileset.py over oracle/chunker.py).
+
+Compared per serialized fileset: SizeBytes, the encoded root index.Index of the additive and
+deletive indexes (which pins, through Range.ChunkRef, every index chunk's Ref.Id and so every
+entry and every data chunk Ref beneath it), every level-0 index entry (pbutil frame) and the
+chunk sequence of every stream (size, edge, Ref.Id).  Workloads cover memThreshold splits
+(including a Put that ends exactly at the threshold, which leaves an empty entry in the next
+fileset), appends, overwrites, tags, empty files, file and directory deletes, and a multilevel
+index (small index chunking params as a test hook; the reference's own 20-bit index chunking
+is run as well).
+"""
+import numpy as np
+import pytest
+
+from oracle import chunker as Ch
+from oracle import fileset as OF
+from pfs_amd import _lib
+from pfs_amd import fileset as PF
+from pfs_amd.cdc import ChunkParams, synthetic_bytes
+
+pytestmark = pytest.mark.gpu
+
+SMALL = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+# index chunking test hook: small enough for several levels, with avg above the largest entry
+# (an entry >= avg is cut before at every level, so levels would never converge; the
+# reference's 1 MiB avg rules that out)
+SMALL_INDEX = Ch.Params(average_bits=13, seed=0, min=3000, max=60000)
+
+
+def cp(p):
+    return ChunkParams(p.average_bits, p.seed, p.min, p.max)
+
+
+def streams(log):
+    """Per stream: chunk (size, edge, id) sequences and index-entry sequences."""
+    out = {}
+    for e in log:
+        if e[0] == "chunk":
+            out.setdefault(("chunk", e[1], e[2]), []).append(e[3:])
+        else:
+            out.setdefault(("index", e[1]), []).append(e[2])
+    return out
+
+
+def run_both(ops, p, mem_threshold, index_params=None):
+    ow = OF.UnorderedWriter(p, mem_threshold, index_params)
+    st = PF.Storage(0, cp(p), mem_threshold, cp(index_params) if index_params else None)
+    pw = st.new_unordered_writer()
+    for op in ops:
+        if op[0] == "put":
+            ow.put(*op[1:])
+            pw.put(*op[1:])
+        else:
+            ow.delete(*op[1:])
+            pw.delete(*op[1:])
+    want = ow.close()
+    got = pw.close()
+    return want, got, ow.log, pw.events
+
+
+def check(want, got, wlog, glog):
+    assert len(got) == len(want)
+    for i, (w, g) in enumerate(zip(want, got)):
+        assert g.size_bytes == w.size_bytes, i
+        assert (g.num_files, g.num_deletes) == (len(w.files), len(w.deletes)), i
+        ws, gs = streams(wlog[i]), streams(glog[i] if i < len(glog) else [])
+        assert sorted(gs) == sorted(ws), i
+        for k in ws:
+            assert gs[k] == ws[k], (i, k)
+        assert g.additive == w.additive, i
+        assert g.deletive == w.deletive, i
+
+
+def workload(seed, nfiles, max_len, dirs=4):
+    rng = np.random.default_rng(seed)
+    data = synthetic_bytes([0, nfiles * max_len], seed).tobytes()
+    ops, pos = [], 0
+    for i in range(nfiles):
+        n = 0 if i % 11 == 0 else int(rng.integers(1, max_len))
+        path = f"/d{int(rng.integers(0, dirs))}/f{int(rng.integers(0, nfiles)):05d}"
+        tag = ["", "default", "t1", "t2"][int(rng.integers(0, 4))]
+        ops.append(("put", path, tag, bool(rng.integers(0, 4) == 0), data[pos:pos + n]))
+        pos += n
+        if i % 17 == 16:
+            ops.append(("delete", ops[-2][1], ""))
+    return ops, data
+
+
+def test_unordered_writer_many_filesets_multilevel_index():
+    ops, _ = workload(1, 160, 40_000)
+    ops.append(("delete", "/d1/", ""))
+    ops.append(("put", "/d1/again", "", False, b"xyz" * 1000))
+    want, got, wlog, glog = run_both(ops, SMALL, 400_000, SMALL_INDEX)
+    assert len(want) >= 5
+    assert any(e[0] == "chunk" and e[1] == 0 and e[2] >= 2 for log in wlog for e in log), \
+        "no multilevel index"
+    check(want, got, wlog, glog)
+
+
+def test_put_ending_exactly_at_threshold_leaves_empty_entry():
+    data = synthetic_bytes([0, 300_000], 7).tobytes()
+    ops = [("put", "/a", "", False, data[:100_000]), ("put", "/b", "", False, data[100_000:250_000]),
+           ("put", "/c", "", False, data[250_000:300_000])]
+    want, got, wlog, glog = run_both(ops, SMALL, 250_000, SMALL_INDEX)
+    assert ("/b", "default") in want[1].files  # the empty re-Add of io.CopyN's exact fill
+    check(want, got, wlog, glog)
+
+
+def test_large_file_split_across_filesets_reference_index_params():
+    # default data chunking and the reference's own index chunking (avgBits 20, seed = level)
+    data = synthetic_bytes([0, 26 << 20], 9).tobytes()
+    ops = [("put", f"/f{i}", "", False, data[i * (3 << 20):(i + 1) * (3 << 20)]) for i in range(4)]
+    ops.append(("put", "/big", "", False, data[12 << 20:]))
+    want, got, wlog, glog = run_both(ops, Ch.Params(), 10_000_000)
+    assert len(want) == 3
+    check(want, got, wlog, glog)
+
+
+def test_writer_errors_are_sticky():
+    st = PF.Storage(0, cp(SMALL), 100_000, cp(SMALL_INDEX))
+    w = st.new_unordered_writer()
+    w.put("/x", "", False, b"abc")
+    w.close()
+    with pytest.raises(_lib.PfsCdcError):
+        w.put("/y", "", False, b"abc")
