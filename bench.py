@@ -58,10 +58,15 @@ def parse():
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
                          "§8 next row 1) inside the step")
-    ap.add_argument("--path", default="put", choices=["put", "get"],
+    ap.add_argument("--path", default="put", choices=["put", "get", "commit"],
                     help="put: the ingest path (default); get: chunk.Get of the step's chunks "
                          "(verify BLAKE2b of the stored bytes against Ref.Id, ChaCha20 "
-                         "decrypt), §8 next row 3, device-resident in and out")
+                         "decrypt), §8 next row 3, device-resident in and out; commit: the "
+                         "pachd data plane, §8 next rows 1-3: files cut into filesets at "
+                         "--mem-threshold bytes, one chunk.Writer stream per fileset (Annotate "
+                         "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk")
+    ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
+                    help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="steps in flight (one GPU context + input buffer each)")
@@ -221,6 +226,9 @@ def main():
     if args.path == "get":
         return bench_get(args, world, rank, local, dev, chunkers[0], batches[0], offs, total,
                          info, scaling, params, np, torch, dist)
+    if args.path == "commit":
+        return bench_commit(args, world, rank, dev, chunkers[0], batches[0], sizes, total, info,
+                            scaling, params, np, torch, dist)
 
     run(args.warmup, False)
     if world > 1:
@@ -451,6 +459,147 @@ def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, s
     if world > 1:
         dist.destroy_process_group()
     chunker.close()
+
+
+def commit_layout(sizes, mem_threshold):
+    """UnorderedWriter.Put of the files in path order (unordered_writer.go:45-72): the files
+    cut into pieces at every mem_threshold bytes, each run of pieces one serialized fileset.
+    A Put that fills the threshold exactly re-Adds its path empty in the next fileset.
+    Returns (piece sizes, stream_file_begin over pieces)."""
+    pieces, streams = [], [0]
+    avail = mem_threshold
+    for n in sizes:
+        n, pos = int(n), 0
+        pieces.append(0)  # buffer.Add(p, tag)
+        while True:  # io.CopyN(w, r, memAvailable)
+            got = min(avail, n - pos)
+            pieces[-1] += got
+            pos += got
+            eof = got < avail
+            avail -= got
+            if eof:
+                break
+            if avail == 0:  # serialize, then re-Add the same path
+                streams.append(len(pieces))
+                avail = mem_threshold
+                pieces.append(0)
+    if streams[-1] != len(pieces):  # Close serializes the rest
+        streams.append(len(pieces))
+    return pieces, streams
+
+
+def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scaling, params,
+                 np, torch, dist):
+    """pachd data plane on the step's files: pieces / filesets (commit_layout), CDC + DataRef
+    hashes (one scan of all pieces), chunk formation per fileset stream (pfscdc_form_chunks),
+    chunk.Create of every formed chunk (pfscdc_create_refs: content hash of multi-DataRef
+    chunks, dek, ChaCha20 + BLAKE2b of the ciphertext)."""
+    pieces, streams = commit_layout(sizes, args.mem_threshold)
+    poffs = np.zeros(len(pieces) + 1, dtype=np.uint64)
+    poffs[1:] = np.cumsum(np.asarray(pieces, dtype=np.uint64))
+    assert int(poffs[-1]) == total
+    chunker.set_ref_ids(False)
+    acc = {"scan": 0.0, "hash": 0.0, "total": 0.0, "create": 0.0, "host_form_ms": 0.0}
+    last = {}
+
+    def step(record):
+        res = chunker.scan(data, poffs)
+        if record:
+            t = chunker.timings()
+            for k in ("scan", "hash", "total"):
+                acc[k] += t[k]
+        h0 = time.perf_counter()
+        coffs, hashes, known = chunker.form_chunks(streams)
+        if record:
+            acc["host_form_ms"] += (time.perf_counter() - h0) * 1e3
+        refs, chash = chunker.create_refs(data, coffs, hashes, known)
+        if record:
+            acc["create"] += chunker.last_create_ms()
+        last.update(res=res, coffs=coffs, known=known, refs=refs)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    bytes_step = total
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        bytes_step = int(bt.item())
+    K = max(args.steps, 1)
+    avg = {k: v / K for k, v in acc.items()}
+    coffs, known = last["coffs"], last["known"]
+    nch = len(coffs) - 1
+    info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
+                         "chunk.Create)", "mem_threshold": args.mem_threshold,
+                 "filesets_per_step": len(streams) - 1, "pieces_per_step": len(pieces),
+                 "chunks_per_step": nch, "multi_dataref_chunks": int(nch - int(known.sum()))})
+    ms = avg["create"]
+    ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    out = {
+        "metric": "GiB/s device-resident pachd commit data plane (CDC + DataRef hashes + "
+                  "chunk formation + chunk.Create Ref.Id)",
+        "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
+        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                     "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
+                     "kernel": "chunk.Create batch (content hash + dek + ChaCha20/BLAKE2b)"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["parity"] = commit_parity(data, pieces, streams, poffs, last, params, np)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    chunker.close()
+
+
+def commit_parity(data, pieces, streams, poffs, last, params, np):
+    """The first fileset through the CPU oracle: segments (C restatement), the chunk.Writer
+    replay (oracle.chunker), and chunk.Create of a sample of its chunks."""
+    from oracle import chunker as och
+    from oracle import coracle
+
+    f1 = streams[1]
+    nb = int(poffs[f1])
+    host = data[:nb].cpu().numpy()
+    p = och.Params(params.average_bits, params.seed, params.min_chunk, params.max_chunk)
+    segs, begin = coracle.segment_files(host, poffs[:f1 + 1], p, nthreads=16)
+    w = och._SegmentReplayWriter(params=p)
+    for f in range(f1):
+        a = int(poffs[f])
+        w.annotate(och.Annotation(data=f))
+        w.write_segments(host[a:int(poffs[f + 1])].tobytes(),
+                         [(int(s["offset"]), int(s["size"]), bool(s["flags"] & 2))
+                          for s in segs[int(begin[f]):int(begin[f + 1])]])
+    w.close()
+    want = np.concatenate([[0], np.cumsum([len(c.data) for c in w.chunks])]).astype(np.uint64)
+    coffs = last["coffs"]
+    n = len(want) - 1
+    same_cuts = bool(np.array_equal(coffs[:n + 1], want))
+    ok = True
+    idx = np.unique(np.linspace(0, n - 1, min(8, n)).astype(int))
+    for i in idx:
+        rid, dek = och.create_ref_id(w.chunks[i].data)
+        ok &= bytes(last["refs"][i]["id"]) == rid and bytes(last["refs"][i]["dek"]) == dek
+    return {"first_fileset_chunk_offsets_equal_oracle": same_cuts, "chunks": n,
+            "ref_ids_equal_oracle": bool(ok), "ref_ids_checked": int(len(idx))}
 
 
 if __name__ == "__main__":

@@ -145,3 +145,21 @@ def test_c5_dedup_commit_matches_oracle_and_hit_rate(mode):
         distinct = len({host[int(offs[f]):int(offs[f + 1])].tobytes() for f in range(len(sizes))})
         if distinct < len(sizes):  # some pooled file drawn twice -> its segments repeat
             assert bench.hit_rate(res.segments)["segment_hit_rate"] > 0
+
+
+def test_commit_layout_matches_oracle_unordered_writer():
+    # bench.commit_layout = the fileset pieces oracle.fileset.UnorderedWriter produces
+    from oracle import fileset as OF
+    for sizes, thr in [([300, 500, 200, 0, 1000], 400), ([400, 400, 1], 400), ([5, 0, 7], 100),
+                       ([1000], 250)]:
+        pieces, streams = bench.commit_layout(sizes, thr)
+        uw = OF.UnorderedWriter(DEFAULT, thr)
+        uw.serialize = lambda uw=uw: (uw.filesets.append(
+            [len(b) for _, _, b in uw.buffer.walk_additive()]) if not uw.buffer.empty() else None,
+            setattr(uw, "buffer", OF.Buffer()), setattr(uw, "mem_available", uw.mem_threshold))
+        for i, n in enumerate(sizes):
+            uw.put(f"/f{i:04d}", "", True, bytes(n))
+        uw.serialize()
+        want = uw.filesets
+        got = [pieces[a:b] for a, b in zip(streams[:-1], streams[1:])]
+        assert got == want, (sizes, thr)
