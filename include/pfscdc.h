@@ -28,6 +28,8 @@ extern "C" {
 #define PFSCDC_EUNSUPPORTED -4 /* configuration the GPU path does not implement */
 #define PFSCDC_ESTATE -5      /* call order violated (e.g. Write before Annotate) */
 #define PFSCDC_ECALLBACK -6   /* the writer callback returned non-zero */
+#define PFSCDC_ECORRUPT -7    /* a stored chunk failed verification (chunk.Get verifyData) */
+#define PFSCDC_ENOTFOUND -8   /* a chunk id is not in the store */
 
 /* chunk.WithRollingHashConfig(averageBits, seed) + chunk.WithMinMax(min, max)
  * (chunk/option.go:50-64); defaults writer.go:39-44: 23, 1, 1 MB, 20 MB (decimal). */
@@ -135,6 +137,9 @@ int pfscdc_last_get_ms(pfscdc_ctx* ctx, float* ms);
 int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
                        const uint8_t* hash_known, pfscdc_ref* refs);
+/* hashDataRefs (fileset/util.go:149-158): FileInfo.Hash = BLAKE2b-256 over the n concatenated
+ * 32-byte DataRef hashes (host array), computed by the hash kernel. */
+int pfscdc_hash_data_refs(pfscdc_ctx* ctx, const uint8_t* hashes, uint32_t n, uint8_t out[32]);
 /* Device time (ms) of the last chunk.Create batch (pfscdc_create_refs or a writer flush). */
 int pfscdc_last_create_ms(pfscdc_ctx* ctx, float* ms);
 
@@ -188,6 +193,10 @@ typedef struct pfscdc_chunk_ref {
   int32_t edge;          /* Ref.Edge = first || last (writer.go:200) */
   int32_t has_ref;       /* ref below is set (the writer was created with PFSCDC_OPT_REF_IDS) */
   pfscdc_ref ref;        /* Ref.Id / Ref.Dek of the whole chunk (maybeUpload, writer.go:255-271) */
+  int32_t copied;        /* 1: a cheap copy (maybeCheapCopy, writer.go:403-420): no new chunk;
+                            the annotations' DataRefs point into the existing chunk whose
+                            Ref this is (has_ref = 1, chunk_index = -1) */
+  int32_t reserved2;
 } pfscdc_chunk_ref;
 
 typedef struct pfscdc_annotation_out {
@@ -203,6 +212,26 @@ typedef int (*pfscdc_writer_cb)(void* user, const pfscdc_chunk_ref* chunk,
 
 typedef struct pfscdc_writer pfscdc_writer;
 
+/* A DataRef with its chunk's Ref (what fileset indexes store, chunk.proto DataRef). */
+typedef struct pfscdc_full_dataref {
+  pfscdc_ref ref;       /* Ref.Id, Ref.Dek */
+  int64_t ref_size;     /* Ref.SizeBytes */
+  int32_t edge;         /* Ref.Edge */
+  int32_t reserved;
+  pfscdc_dataref data;  /* Hash, OffsetBytes, SizeBytes */
+} pfscdc_full_dataref;
+
+/* In-memory chunk store (the chunk client's object store, keyed by Ref.Id: client.go
+ * Create/Get).  Writers with a store upload the ciphertext of every new chunk (deduplicated
+ * by id) and read chunks back for Copy. */
+typedef struct pfscdc_store pfscdc_store;
+int pfscdc_store_create(pfscdc_store** out);
+int pfscdc_store_destroy(pfscdc_store* s);
+int pfscdc_store_put(pfscdc_store* s, const uint8_t id[32], const void* ctext, uint64_t n);
+int pfscdc_store_get(const pfscdc_store* s, const uint8_t id[32], const void** ctext,
+                     uint64_t* n);
+uint64_t pfscdc_store_count(const pfscdc_store* s);
+
 /* batch_bytes: flush threshold for buffered file bytes (0 = 1 GiB).  If ctx has
  * PFSCDC_OPT_REF_IDS set when the writer is created, every chunk also gets its Ref
  * (pfscdc_create_refs over the assembled chunk bytes, multi-file chunks and chunks that span
@@ -215,6 +244,20 @@ int pfscdc_writer_close(pfscdc_writer* w);                               /* writ
 int64_t pfscdc_writer_chunk_count(const pfscdc_writer* w);               /* writer.go:113 */
 int64_t pfscdc_writer_annotation_count(const pfscdc_writer* w);          /* writer.go:107 */
 int pfscdc_writer_destroy(pfscdc_writer* w);
+
+/* The writer's chunk client: Copy reads chunks from store (chunk.Get: verify + decrypt on
+ * the GPU); with upload != 0 every new chunk's ciphertext is stored (needs Ref ids, i.e.
+ * PFSCDC_OPT_REF_IDS on the ctx; WithNoUpload = upload 0). */
+int pfscdc_writer_set_store(pfscdc_writer* w, pfscdc_store* store, int upload);
+/* Writer.Copy(dataRef) (writer.go:315-420): consecutive whole-chunk DataRefs at a chunk
+ * boundary are buffered and passed through by reference (cheap copy, a callback with
+ * chunk.copied = 1); anything else is read back and re-rolled like written bytes. */
+int pfscdc_writer_copy(pfscdc_writer* w, const pfscdc_full_dataref* dr);
+/* MergeFileReader.Hash (fileset/merge.go:125-143): a fresh writer on ctx (no upload), one
+ * annotation, Copy of every DataRef, Close; out = BLAKE2b-256 over the resolved DataRefs'
+ * hashes (hashDataRefs, fileset/util.go:149-158). */
+int pfscdc_merge_file_hash(pfscdc_ctx* ctx, pfscdc_store* store, const pfscdc_full_dataref* drs,
+                           uint32_t n, uint8_t out[32]);
 
 /* Chunk formation over a device-resident batch: the chunks chunk.Writer would create
  * (Annotate cut, CDC cuts, Close's last chunk: writer.go:118-130,198-231,423-438) for the

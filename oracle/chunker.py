@@ -111,14 +111,57 @@ class Chunk:
 # Literal restatement of chunk.Writer
 # --------------------------------------------------------------------------------------
 
+def _merge_data_ref(dr1: Optional[DataRef], dr2: DataRef) -> DataRef:   # writer.go:354-363
+    if dr1 is None:
+        return dr2
+    dr1.size_bytes += dr2.size_bytes
+    if dr1.size_bytes == dr1.ref.size_bytes:
+        dr1.hash = dr1.ref.id
+    return dr1
+
+
+def get_chunk(store: dict, ref: Ref) -> bytes:
+    """chunk.Get (transform.go:50-78) with CreateOptions{}: verify Hash(ctext) == Ref.Id
+    (verifyData), ChaCha20-decrypt with Ref.Dek."""
+    ctext = store[ref.id]
+    if blake2b256(ctext) != ref.id:
+        raise ValueError("bad chunk")
+    return chacha20_xor(ref.dek, ctext)
+
+
+def read_data_ref(store: dict, dr: DataRef) -> bytes:
+    """DataReader.Get (reader.go): the referenced slice of the chunk."""
+    return get_chunk(store, dr.ref)[dr.offset_bytes:dr.offset_bytes + dr.size_bytes]
+
+
+def merge_file_hash(store: dict, data_refs: list, params: Params = Params()) -> bytes:
+    """MergeFileReader.Hash (fileset/merge.go:125-143): Copy the file's DataRefs into a fresh
+    writer under one annotation and hash the DataRefs it resolves to (hashDataRefs).  The Go
+    writer there uses the default chunking; ``params`` is a test hook."""
+    resolved = []
+
+    def cb(annotations):
+        if annotations[0].next_data_ref is not None:
+            resolved.append(annotations[0].next_data_ref)
+    w = Writer(cb=cb, params=params, store=store, no_upload=True)
+    w.annotate(Annotation())
+    for dr in data_refs:
+        w.copy(dr)
+    w.close()
+    return file_hash([d.hash for d in resolved])
+
+
 class Writer:
     """``chunk.Writer`` (writer.go:52-438), upload replaced by an in-memory chunk list."""
 
     def __init__(self, cb: Optional[Callable[[list], None]] = None, params: Params = Params(),
-                 with_ref_id: bool = False):
+                 with_ref_id: bool = False, store: Optional[dict] = None, no_upload: bool = False):
         self.p = params
         self.cb = cb
-        self.with_ref_id = with_ref_id
+        self.with_ref_id = with_ref_id or store is not None
+        self.store = store            # the chunk client: Ref.Id -> ciphertext (Copy reads it)
+        self.no_upload = no_upload    # WithNoUpload: Id = Hash(ctext), nothing stored
+        self.buffering = False
         self.hash = buzhash64.Buzhash64(table(params.seed))
         self.annotations: list[Annotation] = []
         self.num_chunk_bytes_annotation = 0
@@ -142,6 +185,7 @@ class Writer:
         self._reset_hash()
 
     def write(self, data: bytes) -> int:                     # writer.go:132-143
+        self._flush_buffer()
         self._roll(memoryview(bytes(data)))
         return len(data)
 
@@ -193,6 +237,8 @@ class Writer:
         ref = Ref(size_bytes=len(chunk), edge=edge, chunk_index=self.chunk_count)
         if self.with_ref_id:
             ref.id, ref.dek = create_ref_id(chunk)
+            if self.store is not None and not self.no_upload and ref.id not in self.store:
+                self.store[ref.id] = chacha20_xor(ref.dek, chunk)
         self.last_ref = ref
         content_hash = blake2b256(chunk)                     # writer.go:240
         offset = 0
@@ -208,9 +254,64 @@ class Writer:
             self.cb(annotations)
 
     def close(self) -> None:                                 # writer.go:423-438
+        self._flush_buffer()
         if self.annotations:
             self.last = True
             self._create_chunk()
+
+    # ---- Copy (writer.go:315-420): buffer whole-chunk data refs, else re-roll their bytes
+
+    def copy(self, dr: DataRef) -> None:
+        self._maybe_buffer_data_ref(dr)
+        self._maybe_cheap_copy()
+
+    def _maybe_buffer_data_ref(self, dr: DataRef) -> None:  # writer.go:325-352
+        last_a = self.annotations[-1]
+        if last_a.next_data_ref is not None and last_a.next_data_ref.offset_bytes != 0:
+            self._flush_buffer()
+        if not self.buffering:
+            # only at a chunk split point, for a non-edge chunk, from its first byte
+            if len(self.buf) != 0 or dr.ref.edge or dr.offset_bytes != 0:
+                self._flush_data_ref(dr)
+                return
+        else:
+            prev = self._prev_data_ref()
+            if prev.ref.id != dr.ref.id or prev.offset_bytes + prev.size_bytes != dr.offset_bytes:
+                self._flush_buffer()
+                self._flush_data_ref(dr)
+                return
+        last_a.next_data_ref = _merge_data_ref(last_a.next_data_ref, dr)
+        self.buffering = True
+
+    def _prev_data_ref(self) -> DataRef:                     # writer.go:365-372
+        for a in reversed(self.annotations):
+            if a.next_data_ref is not None:
+                return a.next_data_ref
+        raise RuntimeError("no previous data ref")
+
+    def _flush_buffer(self) -> None:                         # writer.go:374-392
+        if not self.buffering:
+            return
+        annotations, self.annotations = self.annotations, []
+        for a in annotations:
+            self.annotate(Annotation(data=a.data))
+            self.annotation_count -= 1
+            if a.next_data_ref is not None:
+                self._flush_data_ref(a.next_data_ref)
+        self.buffering = False
+
+    def _flush_data_ref(self, dr: DataRef) -> None:          # writer.go:394-401 (DataReader.Get)
+        self._roll(memoryview(read_data_ref(self.store, dr)))
+
+    def _maybe_cheap_copy(self) -> None:                     # writer.go:403-420
+        if not self.buffering:
+            return
+        last = self.annotations[-1].next_data_ref
+        if last.offset_bytes + last.size_bytes == last.ref.size_bytes:
+            annotations = self._split_annotations()
+            if self.cb is not None:
+                self.cb(annotations)
+            self.buffering = False
 
 
 # --------------------------------------------------------------------------------------

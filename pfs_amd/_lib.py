@@ -39,6 +39,9 @@ EXPORTED = [
     "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
     "pfscdc_uw_create", "pfscdc_uw_put", "pfscdc_uw_delete", "pfscdc_uw_close",
     "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_path_clean",
+    "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
+    "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
+    "pfscdc_merge_file_hash",
 ]
 
 
@@ -62,7 +65,13 @@ class RefC(C.Structure):
 
 class ChunkRef(C.Structure):
     _fields_ = [("chunk_index", C.c_uint64), ("size_bytes", C.c_int64), ("edge", C.c_int32),
-                ("has_ref", C.c_int32), ("ref", RefC)]
+                ("has_ref", C.c_int32), ("ref", RefC), ("copied", C.c_int32),
+                ("reserved2", C.c_int32)]
+
+
+class FullDataRef(C.Structure):
+    _fields_ = [("ref", RefC), ("ref_size", C.c_int64), ("edge", C.c_int32),
+                ("reserved", C.c_int32), ("data", DataRef)]
 
 
 class AnnotationOut(C.Structure):
@@ -86,7 +95,7 @@ class FilesetInfo(C.Structure):
 EV_CHUNK, EV_INDEX = 1, 2
 UW_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(UwEvent))
 
-assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32 and C.sizeof(ChunkRef) == 88
+assert C.sizeof(Segment) == 56 and C.sizeof(Params) == 32 and C.sizeof(ChunkRef) == 96 and C.sizeof(FullDataRef) == 128
 
 WRITER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(ChunkRef), C.POINTER(AnnotationOut),
                         C.c_uint32)
@@ -188,6 +197,15 @@ def load() -> C.CDLL:
             "pfscdc_uw_fileset": (i32, [vp, u32, P(FilesetInfo)]),
             "pfscdc_uw_destroy": (i32, [vp]),
             "pfscdc_path_clean": (i32, [C.c_char_p, i32, C.c_char_p, u64]),
+            "pfscdc_hash_data_refs": (i32, [vp, vp, u32, vp]),
+            "pfscdc_store_create": (i32, [P(vp)]),
+            "pfscdc_store_destroy": (i32, [vp]),
+            "pfscdc_store_put": (i32, [vp, vp, vp, u64]),
+            "pfscdc_store_get": (i32, [vp, vp, P(vp), P(u64)]),
+            "pfscdc_store_count": (u64, [vp]),
+            "pfscdc_writer_set_store": (i32, [vp, vp, i32]),
+            "pfscdc_writer_copy": (i32, [vp, P(FullDataRef)]),
+            "pfscdc_merge_file_hash": (i32, [vp, vp, P(FullDataRef), u32, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -95,12 +95,62 @@ def with_no_upload() -> WriterOption:
     return opt
 
 
-class Storage:
-    """``chunk.Storage`` restricted to the writer side, bound to one GPU."""
+class ChunkStore:
+    """The chunk client's object store (in memory, keyed by Ref.Id; pfscdc_store)."""
 
-    def __init__(self, device: int = 0, batch_bytes: int = DEFAULT_BATCH_BYTES):
+    def __init__(self):
+        self.lib = _lib.load()
+        s = C.c_void_p()
+        rc = self.lib.pfscdc_store_create(C.byref(s))
+        if rc:
+            raise _lib.PfsCdcError(rc, "pfscdc_store_create")
+        self._s = s
+
+    def __len__(self) -> int:
+        return self.lib.pfscdc_store_count(self._s)
+
+    def get(self, ref_id: bytes) -> bytes:
+        p, n = C.c_void_p(), C.c_uint64()
+        rc = self.lib.pfscdc_store_get(self._s, ref_id, C.byref(p), C.byref(n))
+        if rc:
+            raise KeyError(ref_id.hex())
+        return C.string_at(p, n.value) if n.value else b""
+
+    def put(self, ref_id: bytes, ctext: bytes) -> None:
+        rc = self.lib.pfscdc_store_put(self._s, ref_id, ctext, len(ctext))
+        if rc:
+            raise _lib.PfsCdcError(rc, "pfscdc_store_put")
+
+    def __del__(self):
+        try:
+            if getattr(self, "_s", None):
+                self.lib.pfscdc_store_destroy(self._s)
+                self._s = None
+        except Exception:
+            pass
+
+
+def _full(dr: DataRef) -> _lib.FullDataRef:
+    f = _lib.FullDataRef()
+    C.memmove(f.ref.id, dr.ref.id, 32)
+    C.memmove(f.ref.dek, dr.ref.dek, 32)
+    f.ref_size = dr.ref.size_bytes
+    f.edge = int(dr.ref.edge)
+    C.memmove(f.data.hash, dr.hash, 32)
+    f.data.offset_bytes = dr.offset_bytes
+    f.data.size_bytes = dr.size_bytes
+    return f
+
+
+class Storage:
+    """``chunk.Storage`` bound to one GPU; ``store`` is its chunk client (Copy reads chunks
+    back from it, writers without ``with_no_upload()`` upload into it)."""
+
+    def __init__(self, device: int = 0, batch_bytes: int = DEFAULT_BATCH_BYTES,
+                 store: Optional[ChunkStore] = None):
         self.device = device
         self.batch_bytes = batch_bytes
+        self.store = store
 
     def new_writer(self, name: str, cb: Optional[Callable[[list], None]],
                    *opts: WriterOption) -> "Writer":
@@ -109,11 +159,12 @@ class Storage:
         cfg = _WriterConfig()
         for o in opts:
             o(cfg)
-        return Writer(cfg, cb, self.device, self.batch_bytes)
+        return Writer(cfg, cb, self.device, self.batch_bytes, self.store)
 
 
 class Writer:
-    def __init__(self, cfg: _WriterConfig, cb, device: int, batch_bytes: int):
+    def __init__(self, cfg: _WriterConfig, cb, device: int, batch_bytes: int,
+                 store: Optional[ChunkStore] = None):
         from .cdc import Chunker
 
         self.lib = _lib.load()
@@ -130,11 +181,16 @@ class Writer:
         if rc:
             raise _lib.PfsCdcError(rc, "pfscdc_writer_create")
         self._w = w
+        self._store = store
+        if store is not None:
+            upload = cfg.ref_ids and not cfg.no_upload
+            self._check(self.lib.pfscdc_writer_set_store(w, store._s, int(upload)), "set_store")
 
     def _on_chunk(self, _user, chunk_p, anns_p, n) -> int:
         try:
             ch = chunk_p.contents
-            ref = Ref(size_bytes=ch.size_bytes, edge=bool(ch.edge), chunk_index=ch.chunk_index)
+            ref = Ref(size_bytes=ch.size_bytes, edge=bool(ch.edge),
+                      chunk_index=-1 if ch.copied else ch.chunk_index)
             if ch.has_ref:
                 ref.id, ref.dek = bytes(ch.ref.id), bytes(ch.ref.dek)
             out = []
@@ -172,6 +228,11 @@ class Writer:
         self._check(self.lib.pfscdc_writer_write(self._w, buf, len(buf)), "Write")
         return len(buf)
 
+    def copy(self, data_ref: DataRef) -> None:
+        """Writer.Copy (writer.go:315-420)."""
+        f = _full(data_ref)
+        self._check(self.lib.pfscdc_writer_copy(self._w, C.byref(f)), "Copy")
+
     def close(self) -> None:
         self._check(self.lib.pfscdc_writer_close(self._w), "Close")
 
@@ -190,3 +251,35 @@ class Writer:
                 self._chunker.close()
         except Exception:
             pass
+
+
+def hash_data_refs(hashes, device: int = 0, params: ChunkParams = ChunkParams()) -> bytes:
+    """hashDataRefs (fileset/util.go:149-158) on the GPU: FileInfo.Hash of a file's DataRefs."""
+    from .cdc import Chunker
+    c = Chunker(params, device)
+    buf = b"".join(bytes(h) for h in hashes)
+    out = (C.c_uint8 * 32)()
+    rc = c.lib.pfscdc_hash_data_refs(c.ctx, buf, len(buf) // 32, out)
+    c.close()
+    if rc:
+        raise _lib.PfsCdcError(rc, "hash_data_refs")
+    return bytes(out)
+
+
+def merge_file_hash(store: ChunkStore, data_refs: list, device: int = 0,
+                    params: ChunkParams = ChunkParams()) -> bytes:
+    """MergeFileReader.Hash (fileset/merge.go:125-143): re-chunk a file's DataRefs through a
+    fresh writer (cheap copies where whole chunks line up) and hash the resolved DataRefs.
+    The Go writer there uses the default chunking; ``params`` is a test hook."""
+    from .cdc import Chunker
+    c = Chunker(params, device)
+    arr = (_lib.FullDataRef * max(1, len(data_refs)))()
+    for i, d in enumerate(data_refs):
+        arr[i] = _full(d)
+    out = (C.c_uint8 * 32)()
+    rc = c.lib.pfscdc_merge_file_hash(c.ctx, store._s, arr, len(data_refs), out)
+    msg = c.lib.pfscdc_last_error(c.ctx)
+    c.close()
+    if rc:
+        raise _lib.PfsCdcError(rc, f"merge_file_hash: {msg.decode() if msg else ''}")
+    return bytes(out)

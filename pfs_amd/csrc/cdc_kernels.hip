@@ -900,7 +900,8 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 
 // MODE kModeHash:  DataRef.Hash = BLAKE2b-256(segment) into segs[].hash.
 // MODE kModeRefId: Ref.Id = BLAKE2b-256(ChaCha20_dek(segment)) into refs[].id, dek read from
-//   refs[].dek (chunk.Create with CreateOptions{}: transform.go:26-46,173-188, client.go:57).
+//   refs[].dek (chunk.Create with CreateOptions{}: transform.go:26-46,173-188, client.go:57);
+//   with out != nullptr the ciphertext (the object chunk.Create uploads) is stored there too.
 //   The keystream for the two 64-byte ChaCha20 blocks of each 128-byte message block is
 //   computed by the same quad (lane j = state column j, DPP diagonals, as for BLAKE2b) and
 //   XORed into the LDS message buffer (ds_xor_b32) before the BLAKE2b rounds read it.
@@ -969,6 +970,24 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     else msg_load_full(m0, m1, p);
   };
 
+  auto store_block = [&](uint32_t buf) {  // this lane's 32 bytes of the LDS block -> out
+    const int64_t avail = (int64_t)(L - blk * 128) - 32 * (int64_t)j;
+    if (active && avail > 0) {
+      const uint4 p0 = reinterpret_cast<const uint4*>(my + buf)[0];
+      const uint4 p1 = reinterpret_cast<const uint4*>(my + buf)[1];
+      uint8_t* o = dst_base + blk * 128 + 32 * j;
+      if (avail >= 32) {
+        __builtin_memcpy(o, &p0, 16);
+        __builtin_memcpy(o + 16, &p1, 16);
+      } else {
+        uint8_t tmp[32];
+        __builtin_memcpy(tmp, &p0, 16);
+        __builtin_memcpy(tmp + 16, &p1, 16);
+        for (int64_t k = 0; k < avail; k++) o[k] = tmp[k];
+      }
+    }
+  };
+
   auto step = [&](auto par) -> bool {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     if (!drained) {
@@ -993,7 +1012,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
               key_c = dk[4 + j];
             }
             src = data + offs[seg->file] + seg->offset;
-            if (MODE == kModeGet) dst_base = out + offs[seg->file] + seg->offset;
+            if (MODE != kModeHash && out) dst_base = out + offs[seg->file] + seg->offset;
             nblk = L == 0 ? 1 : (L + 127) / 128;
             blk = 0;
             ha = h0a;
@@ -1027,6 +1046,12 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
           const uint32_t v = last ? ks[w] & keep_bytes(avail - 64 * h - 16 * w - 4 * (int64_t)j) : ks[w];
           __hip_atomic_fetch_xor(dst + 4 * w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+      }
+      if (out) {  // the ciphertext as uploaded (chunk.Create's buf) -> out
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        store_block(cur);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1087,21 +1112,7 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int64_t avail = (int64_t)(L - blk * 128) - 32 * (int64_t)j;  // bytes of this lane's piece
-      if (active && avail > 0) {
-        const uint4 p0 = reinterpret_cast<const uint4*>(my + cur)[0];
-        const uint4 p1 = reinterpret_cast<const uint4*>(my + cur)[1];
-        uint8_t* o = dst_base + blk * 128 + 32 * j;
-        if (avail >= 32) {
-          __builtin_memcpy(o, &p0, 16);
-          __builtin_memcpy(o + 16, &p1, 16);
-        } else {
-          uint8_t tmp[32];
-          __builtin_memcpy(tmp, &p0, 16);
-          __builtin_memcpy(tmp + 16, &p1, 16);
-          for (int64_t k = 0; k < avail; k++) o[k] = tmp[k];
-        }
-      }
+      store_block(cur);
     }
     if (active) {
       blk++;
@@ -1454,7 +1465,7 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          hipStream_t st) {
+                          uint8_t* ctext_out, hipStream_t st) {
   if (max_segments == 0) return hipSuccess;
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
   const uint64_t quads_per_block = kHashBlock / 4;
@@ -1462,7 +1473,7 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
   blake2b_kernel<kModeRefId><<<(unsigned)grid, kHashBlock, 0, st>>>(
-      data, offs, segs, seg_count, order, counter, nbytes, refs, nullptr);
+      data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out);
   return hipGetLastError();
 }
 

@@ -343,7 +343,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0;
   if (c->have_refs && nfiles)
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
-                             c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, st));
+                             c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p,
+                             nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)
@@ -552,6 +553,45 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
                             refs);
 }
 
+int pfscdc_hash_data_refs(pfscdc_ctx* c, const uint8_t* hashes, uint32_t n, uint8_t out[32]) {
+  // hashDataRefs (fileset/util.go:149-158): BLAKE2b-256 of the concatenated DataRef hashes,
+  // one record through the hash kernel
+  if (!c || !out || (n && !hashes)) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "hash_data_refs during a pending scan");
+  const uint64_t nb = 32ull * n;
+  c->scan_valid = false;
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  HIP_OK(c, c->d_data.ensure(nb + 64));
+  HIP_OK(c, c->h_offs.ensure(2));
+  HIP_OK(c, c->h_segs.ensure(1));
+  HIP_OK(c, c->h_seg_begin.ensure(1));
+  HIP_OK(c, c->d_offs.ensure(2));
+  HIP_OK(c, c->d_segs.ensure(1));
+  HIP_OK(c, c->d_order.ensure(1));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  HIP_OK(c, c->d_counts.ensure(4));
+  c->h_offs.p[0] = 0;
+  c->h_offs.p[1] = nb;
+  std::memset(c->h_segs.p, 0, sizeof(pfscdc_segment));
+  c->h_segs.p[0].size = nb;
+  c->h_segs.p[0].flags = PFSCDC_SEG_VALID;
+  c->h_seg_begin.p[0] = 1;
+  if (nb) HIP_OK(c, hipMemcpyAsync(c->d_data.p, hashes, nb, hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment), hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, launch_blake2b(c->d_data.p, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, 1,
+                           c->d_order.p, c->d_qctr.p, c->num_cus, nb, st));
+  HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment), hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  std::memcpy(out, c->h_segs.p[0].hash, 32);
+  c->nsegs = 0;
+  c->have_refs = false;
+  return PFSCDC_OK;
+}
+
 int pfscdc_last_create_ms(pfscdc_ctx* c, float* ms) {
   if (!c || !ms) return PFSCDC_EINVAL;
   *ms = c->create_ms;
@@ -619,7 +659,8 @@ int scan_sync(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_de
 // is not known come first so that one hash pass over records [0, k) computes them; the
 // Ref.Id pass then runs over all n records in its own LPT order.
 int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, const uint64_t* offs,
-                       uint32_t n, uint8_t* hashes, const uint8_t* known, pfscdc_ref* refs) {
+                       uint32_t n, uint8_t* hashes, const uint8_t* known, pfscdc_ref* refs,
+                       uint8_t* ctext_out) {
   if (c->pending) return fail(c, PFSCDC_ESTATE, "create_refs during a pending scan");
   if (n == 0) return PFSCDC_OK;
   c->scan_valid = false;
@@ -665,7 +706,7 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
                              c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
   HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
-                           c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, st));
+                           c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   if (hashes && k)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * k,

@@ -52,9 +52,10 @@ int scan_sync(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_
 // chunk.Create for chunks i = [offs[i], offs[i+1]) of the device buffer data (nbytes valid
 // bytes; offs absolute, offs[0] may be > 0).  hashes (32 B per chunk, may be NULL): in where
 // known[i], else out (Hash(chunk)).  refs: out.  Synchronous.
+// ctext_out (device, nullable): the ciphertexts at the same offsets as data.
 int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
                        const uint64_t* offs, uint32_t n, uint8_t* hashes, const uint8_t* known,
-                       pfscdc_ref* refs);
+                       pfscdc_ref* refs, uint8_t* ctext_out = nullptr);
 int ctx_device(const pfscdc_ctx* ctx);
 uint32_t ctx_options(const pfscdc_ctx* ctx);
 // the last completed scan: still readable (no create_refs / get_chunks since), its files
@@ -83,7 +84,7 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          hipStream_t st);
+                          uint8_t* ctext_out, hipStream_t st);
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
                       int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st);

@@ -10,12 +10,19 @@
 //   maybeUpload       :255-271  chunk.Create(CreateOptions{}) -> Ref.Id/Dek on the GPU
 //                               (pfscdc::create_refs_device) when the ctx asks for refs
 //   processAnnotations:288-312  DataRef{Hash, OffsetBytes, SizeBytes} per piece with size > 0
+//   Copy              :315-420  buffer whole-chunk DataRefs (cheap copy) or re-roll them
 //   Close             :423-438  always emits a last chunk (possibly empty, E1)
-// Hash and seglen reset at every Annotate (writer.go:125-128), so each file's cut positions
-// depend only on its own bytes and whole files can be batched to the GPU; only the
+// The hash and seglen reset at every Annotate and every cut (writer.go:125-128,211), so the
+// bytes after a reset point are scanned as an independent "file" on the GPU; only the
 // cross-file state (open-chunk length, annotation list, first/last) is replayed here, by
 // ChunkFormer, which pfscdc_form_chunks also runs over a device-resident batch.
+//
+// Pending bytes are a list of pending files: a fresh annotation, or a continuation of the
+// last open annotation (bytes written after a flush that stopped at a cut).  A flush scans
+// them and replays the segments; a PARTIAL flush (Copy needs buf.Len()) withholds the last
+// annotation's bytes after its last cut, which stay pending as a continuation.
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -26,12 +33,15 @@ namespace {
 struct PendingFile {
   uint64_t user;
   uint64_t begin;
+  bool cont;  // continues the last open annotation (no Annotate to replay)
 };
 
 struct OpenAnnotation {
   uint64_t user;
-  int64_t size;
+  int64_t size;      // bytes in the open chunk
   uint8_t hash[32];  // hash of the (single) piece this annotation has in the open chunk
+  bool has_next;     // a buffered (Copy) DataRef: Annotation.NextDataRef while buffering
+  pfscdc_full_dataref next;
 };
 
 // One createChunk: the chunk's Ref fields, its annotations (outs[ann_begin, ann_end)) and
@@ -94,7 +104,7 @@ struct ChunkFormer {
     events.push_back(ev);
     const uint64_t last_user = annotations.back().user;
     annotations.clear();
-    annotations.push_back(OpenAnnotation{last_user, 0, {}});
+    annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}});
     first = false;
     open_len = 0;
     open_start = pos;
@@ -103,7 +113,7 @@ struct ChunkFormer {
 
   void annotate(uint64_t user) {  // writer.go:118-130
     if (open_len >= avg && !annotations.empty()) create(false);
-    annotations.push_back(OpenAnnotation{user, 0, {}});
+    annotations.push_back(OpenAnnotation{user, 0, {}, false, {}});
   }
 
   void piece(const pfscdc_segment& s) {  // writeData (+ createChunk at a cut)
@@ -122,12 +132,18 @@ struct ChunkFormer {
 
 }  // namespace
 
+struct pfscdc_store {
+  std::map<std::string, std::string> objects;  // Ref.Id -> ciphertext
+};
+
 struct pfscdc_writer {
   pfscdc_ctx* ctx = nullptr;
   pfscdc_writer_cb cb = nullptr;
   void* user = nullptr;
   uint64_t batch_bytes = 1ULL << 30;
   bool ref_ids = false;
+  pfscdc_store* store = nullptr;      // the chunk client (Copy reads it)
+  bool upload = false;                // Create stores each new chunk's ciphertext
   std::vector<uint8_t> buf;           // pending file bytes
   std::vector<uint8_t> carry;         // ref_ids: bytes of the open chunk from earlier flushes
   std::vector<PendingFile> files;     // pending annotations, in order
@@ -135,9 +151,12 @@ struct pfscdc_writer {
   std::vector<uint64_t> chunk_offs;   // scratch
   std::vector<uint8_t> hashes, known;
   std::vector<pfscdc_ref> refs;
+  std::vector<uint8_t> fetched;       // scratch: a chunk read back for Copy
   uint8_t* d_buf = nullptr;           // ref_ids: carry ++ pending files on the device
+  uint8_t* d_ctext = nullptr;         // upload: ciphertexts, same layout as d_buf
   uint64_t d_cap = 0;
   ChunkFormer cf;
+  bool buffering = false;             // Writer.buffering (Copy)
   bool closed = false;
   int64_t annotation_count = 0;
   int err = 0;                        // sticky (writer.go:145-161)
@@ -145,13 +164,31 @@ struct pfscdc_writer {
 
 namespace {
 
+enum FlushMode { kBatch, kPartial, kFinal };
+
 int set_err(pfscdc_writer* w, int code) {
   if (!w->err) w->err = code;
   return w->err;
 }
 
-// Refs for the chunks formed in this flush (contiguous ranges of d_buf), then the
-// callbacks, serially in chunk order.
+int ensure_device(pfscdc_writer* w, uint64_t need) {
+  if (need <= w->d_cap) return PFSCDC_OK;
+  if (w->d_buf) (void)hipFree(w->d_buf);
+  if (w->d_ctext) (void)hipFree(w->d_ctext);
+  w->d_buf = w->d_ctext = nullptr;
+  w->d_cap = 0;
+  const uint64_t want = need + need / 4;
+  if (hipSetDevice(pfscdc::ctx_device(w->ctx)) != hipSuccess ||
+      hipMalloc((void**)&w->d_buf, want) != hipSuccess)
+    return PFSCDC_ENOMEM;
+  if (w->upload && w->store && hipMalloc((void**)&w->d_ctext, want) != hipSuccess)
+    return PFSCDC_ENOMEM;
+  w->d_cap = want;
+  return PFSCDC_OK;
+}
+
+// Refs (and the upload) for the chunks formed in this flush (contiguous ranges of d_buf),
+// then the callbacks, serially in chunk order.
 int dispatch(pfscdc_writer* w, uint64_t valid) {
   ChunkFormer& cf = w->cf;
   const size_t n = cf.events.size();
@@ -168,8 +205,20 @@ int dispatch(pfscdc_writer* w, uint64_t valid) {
       std::memcpy(&w->hashes[32 * i], ev.hash, 32);
     }
     w->chunk_offs[n] = cf.events[n - 1].end;
+    uint8_t* ct = w->upload && w->store ? w->d_ctext : nullptr;
     rc = pfscdc::create_refs_device(w->ctx, w->d_buf, valid, w->chunk_offs.data(), (uint32_t)n,
-                                    w->hashes.data(), w->known.data(), w->refs.data());
+                                    w->hashes.data(), w->known.data(), w->refs.data(), ct);
+    for (size_t i = 0; i < n && !rc && ct; i++) {  // client.Create: upload unless present
+      const ChunkEvent& ev = cf.events[i];
+      std::string id((const char*)w->refs[i].id, 32);
+      if (w->store->objects.count(id)) continue;
+      std::string obj(ev.end - ev.begin, '\0');
+      if (!obj.empty() &&
+          hipMemcpy(&obj[0], ct + ev.begin, obj.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = PFSCDC_EHIP;
+      else
+        w->store->objects.emplace(std::move(id), std::move(obj));
+    }
     if (rc) {
       cf.events.clear();
       cf.outs.clear();
@@ -191,29 +240,21 @@ int dispatch(pfscdc_writer* w, uint64_t valid) {
   return rc;
 }
 
-// Runs the pending files through the GPU, replays the chunk state machine over their
-// segments (and Close's last chunk if final), then creates refs and calls back.
-int flush(pfscdc_writer* w, bool final) {
+// Runs the pending files through the GPU and replays the chunk state machine over their
+// segments (all of them, or for kPartial up to the last cut of the last annotation), plus
+// Close's last chunk for kFinal; then creates refs and calls back.
+int flush(pfscdc_writer* w, FlushMode mode) {
   const uint32_t nfiles = (uint32_t)w->files.size();
-  if (nfiles == 0 && !final) return PFSCDC_OK;
+  if (nfiles == 0 && mode != kFinal) return PFSCDC_OK;
   ChunkFormer& cf = w->cf;
   const uint64_t nbytes = w->buf.size();
-  uint64_t base = 0;  // device position of the first pending file byte
+  uint64_t base = 0;  // device position of the first pending byte
   if (w->ref_ids) {
     // [carry | files] contiguous on the device, files 16-byte aligned for the scan
     const uint64_t cl = w->carry.size();
     base = (cl + 15) & ~15ULL;
-    const uint64_t need = base + nbytes + 64;
-    if (need > w->d_cap) {
-      if (w->d_buf) (void)hipFree(w->d_buf);
-      w->d_buf = nullptr;
-      w->d_cap = 0;
-      const uint64_t want = need + need / 4;
-      if (hipSetDevice(pfscdc::ctx_device(w->ctx)) != hipSuccess ||
-          hipMalloc((void**)&w->d_buf, want) != hipSuccess)
-        return set_err(w, PFSCDC_ENOMEM);
-      w->d_cap = want;
-    }
+    int rc = ensure_device(w, base + nbytes + 64);
+    if (rc) return set_err(w, rc);
     if ((cl && hipMemcpy(w->d_buf + base - cl, w->carry.data(), cl, hipMemcpyHostToDevice) != hipSuccess) ||
         (nbytes && hipMemcpy(w->d_buf + base, w->buf.data(), nbytes, hipMemcpyHostToDevice) != hipSuccess))
       return set_err(w, PFSCDC_EHIP);
@@ -222,6 +263,9 @@ int flush(pfscdc_writer* w, bool final) {
     cf.open_start = 0;
   }
   cf.pos = base;
+  uint64_t consumed = nbytes;  // pending bytes replayed
+  bool keep_tail = false;
+  uint64_t tail_user = 0;
   if (nfiles) {
     w->offsets.resize(nfiles + 1);
     for (uint32_t f = 0; f < nfiles; f++) w->offsets[f] = w->files[f].begin;
@@ -233,25 +277,187 @@ int flush(pfscdc_writer* w, bool final) {
     const pfscdc_segment* segs = pfscdc_segments(w->ctx);
     const uint64_t* begin = pfscdc_file_segment_begin(w->ctx);
     for (uint32_t f = 0; f < nfiles; f++) {
-      cf.annotate(w->files[f].user);
-      for (uint64_t s = begin[f]; s < begin[f + 1]; s++) cf.piece(segs[s]);
+      if (!w->files[f].cont) cf.annotate(w->files[f].user);
+      uint64_t end = begin[f + 1];
+      if (mode == kPartial && f + 1 == nfiles) {
+        // withhold the bytes after the last cut: the annotation is still being written
+        uint64_t s_end = begin[f];
+        for (uint64_t s = begin[f]; s < end; s++)
+          if (segs[s].flags & PFSCDC_SEG_CUT) s_end = s + 1;
+        consumed = w->offsets[f] + (s_end > begin[f] ? segs[s_end - 1].offset + segs[s_end - 1].size : 0);
+        keep_tail = consumed < nbytes;
+        tail_user = w->files[f].user;
+        end = s_end;
+      }
+      for (uint64_t s = begin[f]; s < end; s++) cf.piece(segs[s]);
     }
   }
-  if (final) cf.close();
+  if (mode == kFinal) cf.close();
   int rc = dispatch(w, base + nbytes);
   if (rc) return rc;
-  if (w->ref_ids) {  // the open chunk's bytes move to the front of the next flush
+  if (w->ref_ids) {  // the open chunk's replayed bytes move to the front of the next flush
     const uint64_t cl = w->carry.size();
     const uint64_t keep_from = cf.open_start;  // >= base - cl
+    const uint64_t keep_to = base + consumed;
     std::vector<uint8_t> next;
     if (keep_from < base) next.assign(w->carry.begin() + (keep_from - (base - cl)), w->carry.end());
     const uint64_t from_buf = keep_from > base ? keep_from - base : 0;
-    next.insert(next.end(), w->buf.begin() + from_buf, w->buf.end());
+    if (keep_to > base + from_buf)
+      next.insert(next.end(), w->buf.begin() + from_buf, w->buf.begin() + (keep_to - base));
     w->carry.swap(next);
   }
   w->files.clear();
-  w->buf.clear();
+  if (keep_tail) {
+    w->buf.erase(w->buf.begin(), w->buf.begin() + consumed);
+    w->files.push_back(PendingFile{tail_user, 0, true});
+  } else {
+    w->buf.clear();
+  }
   return PFSCDC_OK;
+}
+
+// Bytes for the current annotation: into the last pending file, or a continuation of the
+// last open annotation.
+int append_bytes(pfscdc_writer* w, const uint8_t* p, uint64_t n) {
+  if (w->files.empty()) {
+    if (w->cf.annotations.empty()) return set_err(w, PFSCDC_ESTATE);  // Go: index out of range
+    w->files.push_back(PendingFile{w->cf.annotations.back().user, (uint64_t)w->buf.size(), true});
+  }
+  if (n) w->buf.insert(w->buf.end(), p, p + n);
+  return PFSCDC_OK;
+}
+
+// DataReader.Get (reader.go) via chunk.Get on the GPU, then roll (flushDataRef, :394-401).
+int flush_data_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {
+  if (!w->store) return set_err(w, PFSCDC_ESTATE);
+  auto it = w->store->objects.find(std::string((const char*)dr.ref.id, 32));
+  if (it == w->store->objects.end()) return set_err(w, PFSCDC_ENOTFOUND);
+  const std::string& ct = it->second;
+  if (dr.data.offset_bytes < 0 || dr.data.size_bytes < 0 ||
+      (uint64_t)(dr.data.offset_bytes + dr.data.size_bytes) > ct.size())
+    return set_err(w, PFSCDC_EINVAL);
+  w->fetched.resize(ct.size() + 1);
+  const uint64_t offs[2] = {0, (uint64_t)ct.size()};
+  uint8_t ok = 0;
+  int rc = pfscdc_get_chunks(w->ctx, ct.data(), ct.size(), 0, offs, 1, &dr.ref, w->fetched.data(),
+                             0, &ok);
+  if (rc) return set_err(w, rc);
+  if (!ok) return set_err(w, PFSCDC_ECORRUPT);
+  return append_bytes(w, w->fetched.data() + dr.data.offset_bytes, (uint64_t)dr.data.size_bytes);
+}
+
+int pending_annotate(pfscdc_writer* w, uint64_t user) {
+  if (w->buf.size() >= w->batch_bytes) {
+    int rc = flush(w, kBatch);
+    if (rc) return rc;
+  }
+  w->files.push_back(PendingFile{user, (uint64_t)w->buf.size(), false});
+  return PFSCDC_OK;
+}
+
+int flush_buffer(pfscdc_writer* w) {  // writer.go:374-392
+  if (!w->buffering) return PFSCDC_OK;
+  std::vector<OpenAnnotation> anns;
+  anns.swap(w->cf.annotations);
+  for (const OpenAnnotation& a : anns) {
+    int rc = pending_annotate(w, a.user);  // Annotate(copyAnnotation(a)), not counted
+    if (!rc && a.has_next) rc = flush_data_ref(w, a.next);
+    if (rc) return rc;
+  }
+  w->buffering = false;
+  return PFSCDC_OK;
+}
+
+pfscdc_full_dataref merge_data_ref(const pfscdc_full_dataref* dr1, const pfscdc_full_dataref& dr2) {
+  if (!dr1) return dr2;  // writer.go:354-363
+  pfscdc_full_dataref m = *dr1;
+  m.data.size_bytes += dr2.data.size_bytes;
+  if (m.data.size_bytes == m.ref_size) std::memcpy(m.data.hash, m.ref.id, 32);
+  return m;
+}
+
+int maybe_cheap_copy(pfscdc_writer* w) {  // writer.go:403-420
+  if (!w->buffering) return PFSCDC_OK;
+  ChunkFormer& cf = w->cf;
+  const OpenAnnotation& la = cf.annotations.back();
+  if (!la.has_next) return set_err(w, PFSCDC_ESTATE);  // Go: nil NextDataRef dereference
+  const pfscdc_full_dataref& last = la.next;
+  if (last.data.offset_bytes + last.data.size_bytes != last.ref_size) return PFSCDC_OK;
+  pfscdc_chunk_ref ref{};
+  ref.chunk_index = ~0ULL;
+  ref.size_bytes = last.ref_size;
+  ref.edge = last.edge;
+  ref.has_ref = 1;
+  ref.ref = last.ref;
+  ref.copied = 1;
+  std::vector<pfscdc_annotation_out> outs;
+  for (const OpenAnnotation& a : cf.annotations) {
+    pfscdc_annotation_out o{};
+    o.user = a.user;
+    if (a.has_next) {
+      o.has_data_ref = 1;
+      o.data_ref = a.next.data;
+    }
+    outs.push_back(o);
+  }
+  const uint64_t last_user = la.user;
+  cf.annotations.clear();  // splitAnnotations
+  cf.annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}});
+  w->buffering = false;
+  if (w->cb && w->cb(w->user, &ref, outs.data(), (uint32_t)outs.size()) != 0)
+    return set_err(w, PFSCDC_ECALLBACK);
+  return PFSCDC_OK;
+}
+
+int copy_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {  // writer.go:315-352
+  ChunkFormer& cf = w->cf;
+  if (cf.annotations.empty() && w->files.empty()) return set_err(w, PFSCDC_ESTATE);
+  bool stale = false;  // Go merges into the pre-flush lastA, then dereferences nil
+  if (w->buffering) {
+    const OpenAnnotation& la = cf.annotations.back();
+    if (la.has_next && la.next.data.offset_bytes != 0) {
+      int rc = flush_buffer(w);
+      if (rc) return rc;
+      stale = true;
+    }
+  }
+  if (!w->buffering) {
+    if (dr.edge || dr.data.offset_bytes != 0) return flush_data_ref(w, dr);
+    if (!w->files.empty()) {  // buf.Len() needs the pending bytes scanned
+      int rc = flush(w, kPartial);
+      if (rc) return rc;
+    }
+    if (cf.open_len != 0 || !w->buf.empty()) return flush_data_ref(w, dr);
+  } else {
+    const pfscdc_full_dataref* prev = nullptr;  // getPrevDataRef
+    for (auto it = cf.annotations.rbegin(); it != cf.annotations.rend() && !prev; ++it)
+      if (it->has_next) prev = &it->next;
+    if (!prev) return set_err(w, PFSCDC_ESTATE);
+    if (std::memcmp(prev->ref.id, dr.ref.id, 32) != 0 ||
+        prev->data.offset_bytes + prev->data.size_bytes != dr.data.offset_bytes) {
+      int rc = flush_buffer(w);
+      if (rc) return rc;
+      return flush_data_ref(w, dr);
+    }
+  }
+  if (stale || cf.annotations.empty()) return set_err(w, PFSCDC_ESTATE);
+  OpenAnnotation& la = cf.annotations.back();
+  la.next = merge_data_ref(la.has_next ? &la.next : nullptr, dr);
+  la.has_next = true;
+  w->buffering = true;
+  return maybe_cheap_copy(w);
+}
+
+pfscdc_writer* new_writer(pfscdc_ctx* ctx, pfscdc_writer_cb cb, void* user, uint64_t batch_bytes,
+                          bool ref_ids) {
+  pfscdc_writer* w = new pfscdc_writer();
+  w->ctx = ctx;
+  w->cb = cb;
+  w->user = user;
+  if (batch_bytes) w->batch_bytes = batch_bytes;
+  w->ref_ids = ref_ids;
+  w->cf.avg = (int64_t)1 << pfscdc::ctx_params(ctx).average_bits;  // chunkSize.avg, option.go:52
+  return w;
 }
 
 }  // namespace
@@ -261,14 +467,16 @@ extern "C" {
 int pfscdc_writer_create(pfscdc_ctx* ctx, pfscdc_writer_cb cb, void* user, uint64_t batch_bytes,
                          pfscdc_writer** out) {
   if (!ctx || !out) return PFSCDC_EINVAL;
-  pfscdc_writer* w = new pfscdc_writer();
-  w->ctx = ctx;
-  w->cb = cb;
-  w->user = user;
-  if (batch_bytes) w->batch_bytes = batch_bytes;
-  w->ref_ids = (pfscdc::ctx_options(ctx) & PFSCDC_OPT_REF_IDS) != 0;
-  w->cf.avg = (int64_t)1 << pfscdc::ctx_params(ctx).average_bits;  // chunkSize.avg, option.go:52
-  *out = w;
+  *out = new_writer(ctx, cb, user, batch_bytes,
+                    (pfscdc::ctx_options(ctx) & PFSCDC_OPT_REF_IDS) != 0);
+  return PFSCDC_OK;
+}
+
+int pfscdc_writer_set_store(pfscdc_writer* w, pfscdc_store* store, int upload) {
+  if (!w || (upload && !w->ref_ids)) return PFSCDC_EINVAL;
+  if (w->d_cap) return PFSCDC_ESTATE;  // before the first flush
+  w->store = store;
+  w->upload = upload != 0 && store;
   return PFSCDC_OK;
 }
 
@@ -276,33 +484,40 @@ int pfscdc_writer_annotate(pfscdc_writer* w, uint64_t user) {
   if (!w) return PFSCDC_EINVAL;
   if (w->err) return w->err;
   if (w->closed) return set_err(w, PFSCDC_ESTATE);
-  if (w->buf.size() >= w->batch_bytes) {
-    int rc = flush(w, false);
-    if (rc) return rc;
-  }
-  w->files.push_back(PendingFile{user, (uint64_t)w->buf.size()});
   w->annotation_count++;
-  return PFSCDC_OK;
+  if (w->buffering) {  // Annotate does not flush the buffer; the open chunk is empty
+    w->cf.annotations.push_back(OpenAnnotation{user, 0, {}, false, {}});
+    return PFSCDC_OK;
+  }
+  return pending_annotate(w, user);
 }
 
 int pfscdc_writer_write(pfscdc_writer* w, const void* data, uint64_t n) {
   if (!w) return PFSCDC_EINVAL;
   if (w->err) return w->err;
-  if (w->closed || w->files.empty()) return set_err(w, PFSCDC_ESTATE);  // Go: panics
-  if (n) {
-    if (!data) return set_err(w, PFSCDC_EINVAL);
-    const uint8_t* p = (const uint8_t*)data;
-    w->buf.insert(w->buf.end(), p, p + n);
-  }
-  return PFSCDC_OK;
+  if (w->closed || (w->files.empty() && w->cf.annotations.empty()))
+    return set_err(w, PFSCDC_ESTATE);  // Go: panics
+  if (n && !data) return set_err(w, PFSCDC_EINVAL);
+  int rc = flush_buffer(w);
+  if (rc) return rc;
+  return append_bytes(w, (const uint8_t*)data, n);
+}
+
+int pfscdc_writer_copy(pfscdc_writer* w, const pfscdc_full_dataref* dr) {
+  if (!w || !dr) return PFSCDC_EINVAL;
+  if (w->err) return w->err;
+  if (w->closed) return set_err(w, PFSCDC_ESTATE);
+  return copy_ref(w, *dr);
 }
 
 int pfscdc_writer_close(pfscdc_writer* w) {
   if (!w) return PFSCDC_EINVAL;
   if (w->err) return w->err;
   if (w->closed) return PFSCDC_OK;
+  int rc = flush_buffer(w);
+  if (rc) return rc;
   w->closed = true;
-  return flush(w, true);
+  return flush(w, kFinal);
 }
 
 int64_t pfscdc_writer_chunk_count(const pfscdc_writer* w) { return w ? w->cf.chunk_count : 0; }
@@ -313,8 +528,61 @@ int64_t pfscdc_writer_annotation_count(const pfscdc_writer* w) {
 int pfscdc_writer_destroy(pfscdc_writer* w) {
   if (!w) return PFSCDC_EINVAL;
   if (w->d_buf) (void)hipFree(w->d_buf);
+  if (w->d_ctext) (void)hipFree(w->d_ctext);
   delete w;
   return PFSCDC_OK;
+}
+
+int pfscdc_store_create(pfscdc_store** out) {
+  if (!out) return PFSCDC_EINVAL;
+  *out = new pfscdc_store();
+  return PFSCDC_OK;
+}
+
+int pfscdc_store_destroy(pfscdc_store* s) {
+  delete s;
+  return PFSCDC_OK;
+}
+
+int pfscdc_store_put(pfscdc_store* s, const uint8_t id[32], const void* ctext, uint64_t n) {
+  if (!s || !id || (n && !ctext)) return PFSCDC_EINVAL;
+  s->objects.emplace(std::string((const char*)id, 32), std::string((const char*)ctext, n));
+  return PFSCDC_OK;
+}
+
+int pfscdc_store_get(const pfscdc_store* s, const uint8_t id[32], const void** ctext,
+                     uint64_t* n) {
+  if (!s || !id || !ctext || !n) return PFSCDC_EINVAL;
+  auto it = s->objects.find(std::string((const char*)id, 32));
+  if (it == s->objects.end()) return PFSCDC_ENOTFOUND;
+  *ctext = it->second.data();
+  *n = it->second.size();
+  return PFSCDC_OK;
+}
+
+uint64_t pfscdc_store_count(const pfscdc_store* s) { return s ? s->objects.size() : 0; }
+
+int pfscdc_merge_file_hash(pfscdc_ctx* ctx, pfscdc_store* store, const pfscdc_full_dataref* drs,
+                           uint32_t n, uint8_t out[32]) {
+  if (!ctx || !store || !out || (n && !drs)) return PFSCDC_EINVAL;
+  std::vector<uint8_t> resolved;  // the hashes of annotations[0].NextDataRef per callback
+  auto cb = [](void* user, const pfscdc_chunk_ref*, const pfscdc_annotation_out* a,
+               uint32_t na) -> int {
+    if (na && a[0].has_data_ref) {
+      auto* r = (std::vector<uint8_t>*)user;
+      r->insert(r->end(), a[0].data_ref.hash, a[0].data_ref.hash + 32);
+    }
+    return 0;
+  };
+  // WithNoUpload: the new chunks' ids never reach the result, so no Ref pass is run
+  pfscdc_writer* w = new_writer(ctx, cb, &resolved, 0, false);
+  w->store = store;
+  int rc = pfscdc_writer_annotate(w, 0);
+  for (uint32_t i = 0; i < n && !rc; i++) rc = pfscdc_writer_copy(w, &drs[i]);
+  if (!rc) rc = pfscdc_writer_close(w);
+  pfscdc_writer_destroy(w);
+  if (rc) return rc;
+  return pfscdc_hash_data_refs(ctx, resolved.data(), (uint32_t)(resolved.size() / 32), out);
 }
 
 int pfscdc_form_chunks(pfscdc_ctx* ctx, const uint32_t* stream_file_begin, uint32_t nstreams,
