@@ -499,7 +499,8 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
     poffs[1:] = np.cumsum(np.asarray(pieces, dtype=np.uint64))
     assert int(poffs[-1]) == total
     chunker.set_ref_ids(False)
-    acc = {"scan": 0.0, "hash": 0.0, "total": 0.0, "create": 0.0, "host_form_ms": 0.0}
+    acc = {"scan": 0.0, "hash": 0.0, "total": 0.0, "create": 0.0, "create_content_hash": 0.0,
+           "create_ref_id": 0.0, "host_form_ms": 0.0}
     last = {}
 
     def step(record):
@@ -515,6 +516,9 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
         refs, chash = chunker.create_refs(data, coffs, hashes, known)
         if record:
             acc["create"] += chunker.last_create_ms()
+            ct = chunker.last_create_timings()
+            acc["create_content_hash"] += ct["content_hash"]
+            acc["create_ref_id"] += ct["ref_id"]
         last.update(res=res, coffs=coffs, known=known, refs=refs)
 
     for _ in range(args.warmup):

@@ -142,6 +142,8 @@ int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
 int pfscdc_hash_data_refs(pfscdc_ctx* ctx, const uint8_t* hashes, uint32_t n, uint8_t out[32]);
 /* Device time (ms) of the last chunk.Create batch (pfscdc_create_refs or a writer flush). */
 int pfscdc_last_create_ms(pfscdc_ctx* ctx, float* ms);
+/* Its split: out[0] content-hash pass, out[1] Ref.Id pass (order, dek, ChaCha20 + BLAKE2b). */
+int pfscdc_last_create_timings(pfscdc_ctx* ctx, float out[2]);
 
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
  * positions inside dense tiles are reported through the tile marker instead.  Debug/test

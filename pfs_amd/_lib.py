@@ -41,7 +41,7 @@ EXPORTED = [
     "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_path_clean",
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
-    "pfscdc_merge_file_hash",
+    "pfscdc_merge_file_hash", "pfscdc_last_create_timings",
 ]
 
 
@@ -188,6 +188,7 @@ def load() -> C.CDLL:
             "pfscdc_writer_destroy": (i32, [vp]),
             "pfscdc_create_refs": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, vp]),
             "pfscdc_last_create_ms": (i32, [vp, P(C.c_float)]),
+            "pfscdc_last_create_timings": (i32, [vp, P(C.c_float)]),
             "pfscdc_form_chunks": (i32, [vp, P(C.c_uint32), u32, P(u64), vp, vp, u64, P(u64)]),
             "pfscdc_uw_create": (i32, [vp, i64, P(Params), UW_CB, vp, P(vp)]),
             "pfscdc_uw_put": (i32, [vp, C.c_char_p, C.c_char_p, i32, vp, u64]),

@@ -241,6 +241,11 @@ class Chunker:
         self._check(self.lib.pfscdc_last_create_ms(self.ctx, C.byref(ms)), "create_ms")
         return ms.value
 
+    def last_create_timings(self) -> dict:
+        out = (C.c_float * 2)()
+        self._check(self.lib.pfscdc_last_create_timings(self.ctx, out), "create_timings")
+        return {"content_hash": out[0], "ref_id": out[1]}
+
     def last_get_ms(self) -> float:
         ms = C.c_float()
         self._check(self.lib.pfscdc_last_get_ms(self.ctx, C.byref(ms)), "get_ms")

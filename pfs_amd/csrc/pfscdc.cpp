@@ -83,7 +83,8 @@ struct pfscdc_ctx {
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
   float get_ms = 0.f;
-  float create_ms = 0.f;
+  float create_ms = 0.f, create_hash_ms = 0.f;
+  hipEvent_t cev = nullptr;  // create_refs: between the content-hash and the Ref.Id passes
   std::vector<uint32_t> perm;  // create_refs: record -> chunk
   bool have_refs = false;
   bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
@@ -200,6 +201,10 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
       delete c;
       return PFSCDC_EHIP;
     }
+  if (hipEventCreate(&c->cev) != hipSuccess) {
+    delete c;
+    return PFSCDC_EHIP;
+  }
   c->stream = c->own_stream;
   *out = c;
   return PFSCDC_OK;
@@ -232,6 +237,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   if (c->d_table) (void)hipFree(c->d_table);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->cev) (void)hipEventDestroy(c->cev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PFSCDC_OK;
@@ -598,6 +604,13 @@ int pfscdc_last_create_ms(pfscdc_ctx* c, float* ms) {
   return PFSCDC_OK;
 }
 
+int pfscdc_last_create_timings(pfscdc_ctx* c, float out[2]) {
+  if (!c || !out) return PFSCDC_EINVAL;
+  out[0] = c->create_hash_ms;                  // content hashes of multi-DataRef chunks
+  out[1] = c->create_ms - c->create_hash_ms;   // order + dek + ChaCha20/BLAKE2b of ctext
+  return PFSCDC_OK;
+}
+
 int pfscdc_last_get_ms(pfscdc_ctx* c, float* ms) {
   if (!c || !ms) return PFSCDC_EINVAL;
   *ms = c->get_ms;
@@ -704,6 +717,7 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   if (k)
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, k, c->d_order.p,
                              c->d_qctr.p, c->num_cus, nbytes, st));
+  HIP_OK(c, hipEventRecord(c->cev, st));
   HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
   HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
                            c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st));
@@ -724,6 +738,7 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   c->scan_valid = false;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, c->ev[7], c->ev[6]) == hipSuccess) c->create_ms = ms;
+  if (hipEventElapsedTime(&ms, c->ev[7], c->cev) == hipSuccess) c->create_hash_ms = ms;
   return PFSCDC_OK;
 }
 
