@@ -949,6 +949,9 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   const uint64_t h0b = iv_d;
 
   if ((prio_blocks >> 31) && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // A/B: static
+  if ((prio_blocks & 0x3fffffffu) == 0x3fffffffu)  // auto: only when quads refill
+    prio_blocks = (prio_blocks & 0xc0000000u) |
+                  (nseg > (uint64_t)gridDim.x * (kHashBlock / 4) ? 8192u : 0u);
   bool active = false;   // this quad holds a segment
   bool drained = false;  // wave-uniform: the queue is exhausted
   uint64_t L = 0, nblk = 0, blk = 0;
@@ -1444,11 +1447,14 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 
 // Wave issue priority in the hash kernels: a wave raises its priority (s_setprio 2) while
 // one of its quads has more than this many 128-B blocks left, so the long chains of the LPT
-// queue are issued ahead of the short fill-in work.  1 MiB measured best (8192: hash 79 ms
-// vs 96 ms without per 128 GiB; 6000-10000 within 1%, graded levels and a static
-// block-parity priority worse; tools/ab_prio*.sh).  Knobs: PFSCDC_HASH_PRIO (0 = off),
+// queue are issued ahead of the short fill-in work.  It pays when the queue holds more
+// segments than the grid has quads (c2: 44K segments, 32K quads: hash 79 ms vs 96 ms per
+// 128 GiB at 8192 blocks = 1 MiB; 6000-10000 within 1%, graded levels and a static
+// block-parity priority worse) and costs ~4% when every segment starts at once (c4: 132 vs
+// 127 ms), so the default ("auto") enables it at 8192 only when quads will refill
+// (tools/ab_prio*.sh, profiles/r1_prio/).  Knobs: PFSCDC_HASH_PRIO (0 = off, N = fixed),
 // PFSCDC_HASH_PRIO_GRADED, PFSCDC_HASH_PRIO_STATIC (A/B only).
-constexpr uint32_t kHashPrioBlocks = 8192;
+constexpr uint32_t kHashPrioBlocks = 0x3fffffffu;  // auto
 static uint32_t hash_prio_blocks() {
   static const uint32_t v = [] {
     const char* e = getenv("PFSCDC_HASH_PRIO");
