@@ -58,13 +58,15 @@ def parse():
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
                          "§8 next row 1) inside the step")
-    ap.add_argument("--path", default="put", choices=["put", "get", "commit"],
+    ap.add_argument("--path", default="put", choices=["put", "get", "commit", "uw"],
                     help="put: the ingest path (default); get: chunk.Get of the step's chunks "
                          "(verify BLAKE2b of the stored bytes against Ref.Id, ChaCha20 "
                          "decrypt), §8 next row 3, device-resident in and out; commit: the "
                          "pachd data plane, §8 next rows 1-3: files cut into filesets at "
                          "--mem-threshold bytes, one chunk.Writer stream per fileset (Annotate "
                          "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk")
+    ap.add_argument("--uw-bytes", type=int, default=8 << 30,
+                    help="uw: host bytes Put through the UnorderedWriter per step")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
                     help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
@@ -226,6 +228,9 @@ def main():
     if args.path == "get":
         return bench_get(args, world, rank, local, dev, chunkers[0], batches[0], offs, total,
                          info, scaling, params, np, torch, dist)
+    if args.path == "uw":
+        return bench_uw(args, world, rank, dev, chunkers[0], batches[0], sizes, info, scaling,
+                        params, np, torch, dist)
     if args.path == "commit":
         return bench_commit(args, world, rank, dev, chunkers[0], batches[0], sizes, total, info,
                             scaling, params, np, torch, dist)
@@ -572,6 +577,67 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
     if world > 1:
         dist.destroy_process_group()
     chunker.close()
+
+
+def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params, np, torch,
+             dist):
+    """Host-fed pachd write path: the step's first --uw-bytes of files (host memory) Put
+    through the UnorderedWriter (pfs_amd.fileset over pfscdc_uw_*): buffering, 1e9-byte
+    filesets, GPU chunk writers with Ref ids and ciphertext upload off, index writers."""
+    from pfs_amd import fileset as pf
+
+    offs = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
+    nf = int(np.searchsorted(offs, min(args.uw_bytes, int(offs[-1])), side="right")) - 1
+    nf = max(1, nf)
+    nbytes = int(offs[nf])
+    host = data[:nbytes].cpu().numpy()
+    views = [memoryview(host[int(offs[f]):int(offs[f + 1])]) for f in range(nf)]
+    chunker.close()
+    st = pf.Storage(rank % max(1, torch.cuda.device_count()), params, args.mem_threshold)
+
+    def step():
+        w = st.new_unordered_writer()
+        for f in range(nf):
+            w.put("/%016d" % f, "", False, views[f])
+        prims = w.close()
+        return prims, w
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        prims, w = step()
+    elapsed = time.perf_counter() - t0
+    bytes_step = nbytes
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        bt = torch.tensor([nbytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        bytes_step = int(bt.item())
+    K = max(args.steps, 1)
+    nchunks = sum(1 for fs in w.events for e in fs if e[0] == "chunk" and e[1] == -1)
+    info.update({"path": "uw (host-fed UnorderedWriter -> fileset.Writer -> index.Writer)",
+                 "files_per_step": nf, "bytes_per_step": nbytes,
+                 "mem_threshold": args.mem_threshold, "filesets_per_step": len(prims),
+                 "data_chunks_per_step": nchunks})
+    out = {
+        "metric": "GiB/s host-fed pachd write path (Put -> filesets with chunk Refs and "
+                  "multilevel indexes)",
+        "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic bytes in host memory", "config": info,
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def commit_parity(data, pieces, streams, poffs, last, params, np):

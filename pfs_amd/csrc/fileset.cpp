@@ -13,6 +13,7 @@
 //   chunk/chunk.proto, fileset/index/index.proto, chunk/util.go:25-30 (Reference)
 // Every chunk stream (the data writer of a serialized fileset and each index level) is a
 // pfscdc_writer: CDC, BLAKE2b and chunk.Create run on the GPU; this file is the bookkeeping.
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -192,10 +193,9 @@ struct Streams {  // the ctxs of every chunk stream kind; events out
   std::map<int64_t, pfscdc_ctx*> index_ctx;  // by seed (= level)
   pfscdc_uw_cb cb = nullptr;
   void* user = nullptr;
-  uint32_t fileset = 0;
   int err = 0;
 
-  int emit(pfscdc_uw_event& ev) {
+  int emit(pfscdc_uw_event& ev, uint32_t fileset) {
     ev.fileset = fileset;
     if (cb && cb(user, &ev) != 0) return PFSCDC_ECALLBACK;
     return PFSCDC_OK;
@@ -219,6 +219,10 @@ struct Streams {  // the ctxs of every chunk stream kind; events out
 struct IndexWriter;
 constexpr int kMaxIndexLevels = 32;
 
+struct Span {  // bytes [off, off + len) of a fileset's Put arena
+  uint64_t off, len;
+};
+
 struct Level {
   IndexWriter* iw;
   int level;
@@ -233,6 +237,7 @@ struct IndexWriter {  // index/writer.go:27-162
   bool closed = false;
   IndexT* root = nullptr;
   std::vector<std::unique_ptr<IndexT>>* pool;
+  uint32_t fs = 0;  // serialized fileset number (events)
 
   ~IndexWriter() {
     for (auto& l : levels)
@@ -264,7 +269,7 @@ struct IndexWriter {  // index/writer.go:27-162
       ev.index = which;
       ev.bytes = (const uint8_t*)b.data();
       ev.len = b.size();
-      int rc = st->emit(ev);
+      int rc = st->emit(ev, fs);
       if (rc) return rc;
     }
     pfscdc_writer* cw = levels[level]->cw;
@@ -282,7 +287,7 @@ struct IndexWriter {  // index/writer.go:27-162
     ev.index = w->which;
     ev.level = lw->level;
     ev.chunk = *chunk;
-    int rc = w->st->emit(ev);
+    int rc = w->st->emit(ev, w->fs);
     if (rc || n == 0) return rc;
     IndexT* idx = (IndexT*)(uintptr_t)a[0].user;
     const pfscdc_annotation_out* dr = &a[0];
@@ -336,10 +341,14 @@ struct FilesetWriter {  // fileset/writer.go:21-182
   pfscdc_writer* cw = nullptr;
   IndexT *idx = nullptr, *delete_idx = nullptr, *last_idx = nullptr;
   FilesetInfo info;
+  uint32_t fs;
   int err = 0;
 
-  explicit FilesetWriter(Streams* s) : st(s), additive{s, 0, {}, false, nullptr, &pool},
-                                       deletive{s, 1, {}, false, nullptr, &pool} {}
+  FilesetWriter(Streams* s, uint32_t fileset) : st(s), additive{s, 0, {}, false, nullptr, &pool},
+                                                deletive{s, 1, {}, false, nullptr, &pool},
+                                                fs(fileset) {
+    additive.fs = deletive.fs = fileset;
+  }
   ~FilesetWriter() {
     if (cw) pfscdc_writer_destroy(cw);
   }
@@ -360,15 +369,20 @@ struct FilesetWriter {  // fileset/writer.go:21-182
     return pool.back().get();
   }
 
-  int add(const std::string& path, const std::string& tag, const std::string& data) {
+  // Add(path, tag, r) with r = the concatenation of spans of base (kept alive by the caller
+  // until the data writer closes)
+  int add(const std::string& path, const std::string& tag, const uint8_t* base,
+          const std::vector<Span>& spans) {
     IndexT* x = make(path, tag);
     int rc = check_path(idx, x);
     if (rc) return rc;
     idx = x;
     info.files.emplace_back(path, tag);
     rc = pfscdc_writer_annotate(cw, (uint64_t)(uintptr_t)x);
-    if (!rc) rc = pfscdc_writer_write(cw, data.data(), data.size());
-    info.size_bytes += (int64_t)data.size();
+    for (const Span& sp : spans) {
+      if (!rc) rc = pfscdc::writer_write_span(cw, base + sp.off, sp.len);
+      info.size_bytes += (int64_t)sp.len;
+    }
     return rc;
   }
 
@@ -388,7 +402,7 @@ struct FilesetWriter {  // fileset/writer.go:21-182
     ev.kind = PFSCDC_EV_CHUNK;
     ev.index = -1;
     ev.chunk = *chunk;
-    int rc = w->st->emit(ev);
+    int rc = w->st->emit(ev, w->fs);
     if (rc) return rc;
     const RefT ref = ref_of(chunk);
     for (uint32_t i = 0; i < n; i++) {
@@ -413,7 +427,11 @@ struct FilesetWriter {  // fileset/writer.go:21-182
 
   int close() {
     int rc = pfscdc_writer_close(cw);
-    if (rc) return rc;
+    return rc ? rc : finish();
+  }
+
+  int finish() {  // Close after the data writer closed: the last entry, then the indexes
+    int rc = PFSCDC_OK;
     if (last_idx) {
       rc = additive.write_index(last_idx, 0);
       if (rc) return rc;
@@ -434,11 +452,20 @@ struct FilesetWriter {  // fileset/writer.go:21-182
   }
 };
 
-struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFiles does
-  std::map<std::string, std::map<std::string, std::string>> additive;
-  std::map<std::string, std::set<std::string>> deletive;
+// Host bytes of one fileset's Puts, appended in arrival order (a Put copies into it once);
+// the Buffer keeps each file as spans of it and the fileset's chunk writer uploads the spans
+// straight from here in path order.  Recycled through the writer's pool.
+struct Arena {
+  std::unique_ptr<uint8_t[]> p;
+  uint64_t cap = 0, used = 0;
+};
 
-  std::string& add(const std::string& path0, const std::string& tag) {
+struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFiles does
+  std::map<std::string, std::map<std::string, std::vector<Span>>> additive;
+  std::map<std::string, std::set<std::string>> deletive;
+  std::unique_ptr<Arena> arena;
+
+  std::vector<Span>& add(const std::string& path0, const std::string& tag) {
     return additive[clean(path0, false)][tag];
   }
   void del(const std::string& path0, const std::string& tag) {
@@ -464,6 +491,15 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   int64_t mem_available = 1000000000;
   Buffer buffer;
   std::vector<FilesetInfo> filesets;
+  // Serialized buffers waiting for the GPU: up to inflight_bytes of them are written
+  // together (one scan and one chunk.Create for all their data streams).  The output equals
+  // serializing one at a time; each fileset's chunk stream is independent.
+  std::vector<Buffer> pending;
+  std::vector<std::unique_ptr<Arena>> pool;  // arenas of written filesets, for reuse
+  uint64_t pending_bytes = 0, inflight_bytes = 8ull << 30;
+  std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
+                        std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
+  uint32_t next_fileset = 0;
   bool closed = false;
   int err = 0;
 
@@ -472,34 +508,83 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     return err;
   }
 
+  std::unique_ptr<Arena> new_arena() {
+    if (!pool.empty()) {
+      std::unique_ptr<Arena> a = std::move(pool.back());
+      pool.pop_back();
+      a->used = 0;
+      return a;
+    }
+    auto a = std::make_unique<Arena>();
+    a->cap = (uint64_t)mem_threshold;  // a Buffer never holds more than memThreshold bytes
+    a->p.reset(new (std::nothrow) uint8_t[a->cap]);
+    if (!a->p) return nullptr;
+    return a;
+  }
+
   int serialize() {  // unordered_writer.go:83-122
     if (buffer.empty()) return PFSCDC_OK;
-    FilesetWriter fw(&st);
-    int rc = fw.open();
+    std::vector<std::pair<std::string, std::string>> files, deletes;
     for (auto& p : buffer.additive)
-      for (auto& t : p.second)
-        if (!rc) rc = fw.add(p.first, t.first, t.second);
+      for (auto& t : p.second) files.emplace_back(p.first, t.first);
     for (auto& p : buffer.deletive)
-      for (auto& t : p.second)
-        if (!rc) rc = fw.del(p.first, t);
-    if (!rc) rc = fw.close();
-    if (rc) return rc;
-    filesets.push_back(std::move(fw.info));
+      for (auto& t : p.second) deletes.emplace_back(p.first, t);
+    keys.emplace_back(std::move(files), std::move(deletes));
+    pending_bytes += buffer.arena ? buffer.arena->used : 0;
+    pending.push_back(std::move(buffer));
     buffer = Buffer();
     mem_available = mem_threshold;
-    st.fileset++;
-    return PFSCDC_OK;
+    next_fileset++;
+    return pending_bytes >= inflight_bytes ? flush_pending() : PFSCDC_OK;
+  }
+
+  int flush_pending() {  // fileset.Writer for each pending buffer, data streams together
+    if (pending.empty()) return PFSCDC_OK;
+    const uint32_t fs0 = next_fileset - (uint32_t)pending.size();
+    std::vector<std::unique_ptr<FilesetWriter>> fws;
+    std::vector<pfscdc_writer*> cws;
+    int rc = PFSCDC_OK;
+    for (size_t i = 0; i < pending.size() && !rc; i++) {
+      fws.push_back(std::make_unique<FilesetWriter>(&st, fs0 + (uint32_t)i));
+      FilesetWriter& fw = *fws.back();
+      rc = fw.open();
+      const uint8_t* base = pending[i].arena ? pending[i].arena->p.get() : nullptr;
+      for (auto& p : pending[i].additive)
+        for (auto& t : p.second)
+          if (!rc) rc = fw.add(p.first, t.first, base, t.second);
+      for (auto& p : pending[i].deletive)
+        for (auto& t : p.second)
+          if (!rc) rc = fw.del(p.first, t);
+      cws.push_back(fw.cw);
+    }
+    if (!rc) rc = pfscdc::writers_close_group(cws.data(), cws.size());
+    for (size_t i = 0; i < fws.size() && !rc; i++) {
+      rc = fws[i]->finish();
+      if (!rc) filesets.push_back(std::move(fws[i]->info));
+    }
+    for (Buffer& b : pending)
+      if (b.arena) pool.push_back(std::move(b.arena));
+    pending.clear();
+    pending_bytes = 0;
+    return rc;
   }
 
   int put(const std::string& p, std::string tag, bool append, const uint8_t* data, uint64_t n) {
     if (tag.empty()) tag = "default";
     if (!append) buffer.del(p, tag);
-    std::string* w = &buffer.add(p, tag);
+    std::vector<Span>* w = &buffer.add(p, tag);
     uint64_t pos = 0;
     for (;;) {  // io.CopyN(w, r, memAvailable): EOF iff fewer than memAvailable bytes were left
       const uint64_t want = (uint64_t)mem_available;
       const uint64_t got = std::min<uint64_t>(want, n - pos);
-      w->append((const char*)data + pos, got);
+      if (got) {
+        if (!buffer.arena && !(buffer.arena = new_arena())) return PFSCDC_ENOMEM;
+        Arena& a = *buffer.arena;
+        std::memcpy(a.p.get() + a.used, data + pos, got);
+        if (!w->empty() && w->back().off + w->back().len == a.used) w->back().len += got;
+        else w->push_back(Span{a.used, got});
+        a.used += got;
+      }
       pos += got;
       mem_available -= (int64_t)got;
       if (got < want) return PFSCDC_OK;
@@ -522,9 +607,9 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     // merged view of the serialized filesets (merge.go: a (path, tag) group is live iff its
     // last stream, deletive before additive within a fileset, is additive)
     std::map<std::pair<std::string, std::string>, bool> live;
-    for (const FilesetInfo& fs : filesets) {
-      for (auto& k : fs.deletes) live[k] = false;
-      for (auto& k : fs.files) live[k] = true;
+    for (const auto& fs : keys) {  // serialized filesets, written or pending
+      for (auto& k : fs.second) live[k] = false;
+      for (auto& k : fs.first) live[k] = true;
     }
     for (auto& kv : live)
       if (kv.second && kv.first.first.compare(0, p.size(), p) == 0) buffer.del(kv.first.first, tag);
@@ -551,6 +636,7 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
     w->st.index_params.seed = 0;
   }
   if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
+  if (const char* e = getenv("PFSCDC_UW_INFLIGHT")) w->inflight_bytes = strtoull(e, nullptr, 10);
   *out = w;
   return PFSCDC_OK;
 }
@@ -578,6 +664,7 @@ int pfscdc_uw_close(pfscdc_uwriter* w) {
   if (w->closed) return PFSCDC_OK;
   w->closed = true;
   int rc = w->serialize();
+  if (!rc) rc = w->flush_pending();
   return rc ? w->fail(rc) : PFSCDC_OK;
 }
 

@@ -57,6 +57,10 @@ int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
                        const uint64_t* offs, uint32_t n, uint8_t* hashes, const uint8_t* known,
                        pfscdc_ref* refs, uint8_t* ctext_out = nullptr);
 int ctx_device(const pfscdc_ctx* ctx);
+// pfscdc_writer_close of n writers on one ctx with one scan and one chunk.Create pass
+int writers_close_group(pfscdc_writer* const* ws, size_t n);
+// a write whose bytes stay owned by the caller until the writer flushes or closes
+int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n);
 uint32_t ctx_options(const pfscdc_ctx* ctx);
 // the last completed scan: still readable (no create_refs / get_chunks since), its files
 bool ctx_scan_valid(const pfscdc_ctx* ctx);

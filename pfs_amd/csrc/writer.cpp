@@ -21,6 +21,9 @@
 // last open annotation (bytes written after a flush that stopped at a cut).  A flush scans
 // them and replays the segments; a PARTIAL flush (Copy needs buf.Len()) withholds the last
 // annotation's bytes after its last cut, which stay pending as a continuation.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -145,6 +148,10 @@ struct pfscdc_writer {
   pfscdc_store* store = nullptr;      // the chunk client (Copy reads it)
   bool upload = false;                // Create stores each new chunk's ciphertext
   std::vector<uint8_t> buf;           // pending file bytes
+  // pending bytes held by the caller instead (writer_write_span: a fileset's Put arena);
+  // their concatenation replaces buf, which stays empty while spans are pending
+  std::vector<std::pair<const uint8_t*, uint64_t>> spans;
+  uint64_t span_bytes = 0;
   std::vector<uint8_t> carry;         // ref_ids: bytes of the open chunk from earlier flushes
   std::vector<PendingFile> files;     // pending annotations, in order
   std::vector<uint64_t> offsets;      // scratch
@@ -187,6 +194,37 @@ int ensure_device(pfscdc_writer* w, uint64_t need) {
   return PFSCDC_OK;
 }
 
+// The callbacks of the chunks formed in this flush, serially in chunk order (refs in w->refs).
+int callbacks(pfscdc_writer* w) {
+  ChunkFormer& cf = w->cf;
+  int rc = PFSCDC_OK;
+  for (size_t i = 0; i < cf.events.size() && !rc; i++) {
+    ChunkEvent& ev = cf.events[i];
+    if (w->ref_ids) {
+      ev.ref.has_ref = 1;
+      ev.ref.ref = w->refs[i];
+    }
+    if (w->cb && w->cb(w->user, &ev.ref, cf.outs.data() + ev.ann_begin,
+                       (uint32_t)(ev.ann_end - ev.ann_begin)) != 0)
+      rc = set_err(w, PFSCDC_ECALLBACK);
+  }
+  cf.events.clear();
+  cf.outs.clear();
+  return rc;
+}
+
+// client.Create's upload of chunk i's ciphertext (device ct + [begin, end)) unless present.
+int upload(pfscdc_store* st, const pfscdc_ref& ref, const uint8_t* ct, uint64_t begin,
+           uint64_t end) {
+  std::string id((const char*)ref.id, 32);
+  if (st->objects.count(id)) return PFSCDC_OK;
+  std::string obj(end - begin, '\0');
+  if (!obj.empty() && hipMemcpy(&obj[0], ct + begin, obj.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return PFSCDC_EHIP;
+  st->objects.emplace(std::move(id), std::move(obj));
+  return PFSCDC_OK;
+}
+
 // Refs (and the upload) for the chunks formed in this flush (contiguous ranges of d_buf),
 // then the callbacks, serially in chunk order.
 int dispatch(pfscdc_writer* w, uint64_t valid) {
@@ -208,42 +246,31 @@ int dispatch(pfscdc_writer* w, uint64_t valid) {
     uint8_t* ct = w->upload && w->store ? w->d_ctext : nullptr;
     rc = pfscdc::create_refs_device(w->ctx, w->d_buf, valid, w->chunk_offs.data(), (uint32_t)n,
                                     w->hashes.data(), w->known.data(), w->refs.data(), ct);
-    for (size_t i = 0; i < n && !rc && ct; i++) {  // client.Create: upload unless present
-      const ChunkEvent& ev = cf.events[i];
-      std::string id((const char*)w->refs[i].id, 32);
-      if (w->store->objects.count(id)) continue;
-      std::string obj(ev.end - ev.begin, '\0');
-      if (!obj.empty() &&
-          hipMemcpy(&obj[0], ct + ev.begin, obj.size(), hipMemcpyDeviceToHost) != hipSuccess)
-        rc = PFSCDC_EHIP;
-      else
-        w->store->objects.emplace(std::move(id), std::move(obj));
-    }
+    for (size_t i = 0; i < n && !rc && ct; i++)
+      rc = upload(w->store, w->refs[i], ct, cf.events[i].begin, cf.events[i].end);
     if (rc) {
       cf.events.clear();
       cf.outs.clear();
       return set_err(w, rc);
     }
   }
-  for (size_t i = 0; i < n && !rc; i++) {
-    ChunkEvent& ev = cf.events[i];
-    if (w->ref_ids) {
-      ev.ref.has_ref = 1;
-      ev.ref.ref = w->refs[i];
-    }
-    if (w->cb && w->cb(w->user, &ev.ref, cf.outs.data() + ev.ann_begin,
-                       (uint32_t)(ev.ann_end - ev.ann_begin)) != 0)
-      rc = set_err(w, PFSCDC_ECALLBACK);
-  }
-  cf.events.clear();
-  cf.outs.clear();
-  return rc;
+  return callbacks(w);
 }
 
 // Runs the pending files through the GPU and replays the chunk state machine over their
 // segments (all of them, or for kPartial up to the last cut of the last annotation), plus
 // Close's last chunk for kFinal; then creates refs and calls back.
+// Copies pending caller spans into buf (every path but the grouped close reads buf).
+void materialize(pfscdc_writer* w) {
+  if (w->spans.empty()) return;
+  w->buf.reserve(w->buf.size() + w->span_bytes);
+  for (auto& sp : w->spans) w->buf.insert(w->buf.end(), sp.first, sp.first + sp.second);
+  w->spans.clear();
+  w->span_bytes = 0;
+}
+
 int flush(pfscdc_writer* w, FlushMode mode) {
+  materialize(w);
   const uint32_t nfiles = (uint32_t)w->files.size();
   if (nfiles == 0 && mode != kFinal) return PFSCDC_OK;
   ChunkFormer& cf = w->cf;
@@ -319,6 +346,7 @@ int flush(pfscdc_writer* w, FlushMode mode) {
 // Bytes for the current annotation: into the last pending file, or a continuation of the
 // last open annotation.
 int append_bytes(pfscdc_writer* w, const uint8_t* p, uint64_t n) {
+  materialize(w);
   if (w->files.empty()) {
     if (w->cf.annotations.empty()) return set_err(w, PFSCDC_ESTATE);  // Go: index out of range
     w->files.push_back(PendingFile{w->cf.annotations.back().user, (uint64_t)w->buf.size(), true});
@@ -347,11 +375,11 @@ int flush_data_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {
 }
 
 int pending_annotate(pfscdc_writer* w, uint64_t user) {
-  if (w->buf.size() >= w->batch_bytes) {
+  if (w->spans.empty() && w->buf.size() >= w->batch_bytes) {
     int rc = flush(w, kBatch);
     if (rc) return rc;
   }
-  w->files.push_back(PendingFile{user, (uint64_t)w->buf.size(), false});
+  w->files.push_back(PendingFile{user, (uint64_t)(w->buf.size() + w->span_bytes), false});
   return PFSCDC_OK;
 }
 
@@ -461,6 +489,167 @@ pfscdc_writer* new_writer(pfscdc_ctx* ctx, pfscdc_writer_cb cb, void* user, uint
 }
 
 }  // namespace
+
+namespace pfscdc {
+
+// Close several writers of one ctx with one scan and one chunk.Create pass, equivalent to
+// pfscdc_writer_close on each in order (their chunk streams are independent).  Only for
+// writers that never flushed and buffer no Copy (each fileset's data writer at Close);
+// anything else closes one by one.  Batching keeps enough BLAKE2b chains in flight: one
+// 1e9-byte fileset of ~10 MB files has ~100 chains, far below the ~32K the GPU holds.
+int writers_close_group(pfscdc_writer* const* ws, size_t n) {
+  if (n == 0) return PFSCDC_OK;
+  pfscdc_ctx* ctx = ws[0]->ctx;
+  bool group = n > 1;
+  for (size_t i = 0; i < n && group; i++) {
+    const pfscdc_writer* w = ws[i];
+    group = !w->err && !w->closed && w->ctx == ctx && !w->buffering && w->carry.empty() &&
+            w->d_cap == 0 && w->ref_ids == ws[0]->ref_ids &&
+            (w->upload && w->store) == (ws[0]->upload && ws[0]->store);
+  }
+  if (!group) {
+    for (size_t i = 0; i < n; i++) {
+      int rc = pfscdc_writer_close(ws[i]);
+      if (rc) return rc;
+    }
+    return PFSCDC_OK;
+  }
+  const bool trace = getenv("PFSCDC_TRACE") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const auto t0 = now();
+  // layout: writer i's pending bytes at base[i] (16-B aligned); the alignment gaps are
+  // dummy files whose segments are ignored
+  std::vector<uint64_t> base(n), offsets;
+  std::vector<size_t> first(n);
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t b = (pos + 15) & ~15ULL;
+    if (b > pos) offsets.push_back(pos);
+    base[i] = b;
+    first[i] = offsets.size();
+    for (const PendingFile& f : ws[i]->files) offsets.push_back(b + f.begin);
+    pos = b + ws[i]->buf.size() + ws[i]->span_bytes;
+  }
+  const uint64_t total = pos;
+  const uint32_t nfiles = (uint32_t)offsets.size();
+  offsets.push_back(total);
+  uint8_t *d = nullptr, *dct = nullptr;
+  const bool up = ws[0]->upload && ws[0]->store;
+  int rc = PFSCDC_OK;
+  if (hipSetDevice(ctx_device(ctx)) != hipSuccess || hipMalloc((void**)&d, total + 64) != hipSuccess ||
+      (up && hipMalloc((void**)&dct, total + 64) != hipSuccess))
+    rc = PFSCDC_ENOMEM;
+  for (size_t i = 0; i < n && !rc; i++) {
+    const pfscdc_writer* w = ws[i];
+    uint64_t at = base[i];
+    if (!w->buf.empty() &&
+        hipMemcpy(d + at, w->buf.data(), w->buf.size(), hipMemcpyHostToDevice) != hipSuccess)
+      rc = PFSCDC_EHIP;
+    at += w->buf.size();
+    for (size_t k = 0; k < w->spans.size() && !rc; k++) {
+      const auto& sp = w->spans[k];
+      if (sp.second && hipMemcpy(d + at, sp.first, sp.second, hipMemcpyHostToDevice) != hipSuccess)
+        rc = PFSCDC_EHIP;
+      at += sp.second;
+    }
+  }
+  const auto t1 = now();
+  if (!rc && nfiles) rc = scan_sync(ctx, d, total, 1, offsets.data(), nfiles, 0);
+  const auto t2 = now();
+  // replay every writer over its own files
+  if (!rc) {
+    const pfscdc_segment* segs = pfscdc_segments(ctx);
+    const uint64_t* begin = pfscdc_file_segment_begin(ctx);
+    for (size_t i = 0; i < n; i++) {
+      pfscdc_writer* w = ws[i];
+      ChunkFormer& cf = w->cf;
+      cf.open_start = cf.pos = base[i];
+      for (size_t k = 0; k < w->files.size(); k++) {
+        const size_t g = first[i] + k;
+        if (!w->files[k].cont) cf.annotate(w->files[k].user);
+        for (uint64_t s = begin[g]; s < begin[g + 1]; s++) cf.piece(segs[s]);
+      }
+      cf.close();
+    }
+  }
+  // one chunk.Create over every writer's chunks (gaps between writers are dummy records)
+  const auto t3 = now();
+  if (!rc && ws[0]->ref_ids) {
+    std::vector<uint64_t> coffs;
+    std::vector<uint8_t> hashes, known;
+    std::vector<std::pair<size_t, size_t>> who;  // record -> (writer, event), or gap
+    uint64_t at = 0;
+    for (size_t i = 0; i < n; i++) {
+      for (size_t e = 0; e < ws[i]->cf.events.size(); e++) {
+        const ChunkEvent& ev = ws[i]->cf.events[e];
+        if (ev.begin > at) {  // gap
+          coffs.push_back(at);
+          known.push_back(1);
+          hashes.resize(hashes.size() + 32, 0);
+          who.emplace_back(SIZE_MAX, 0);
+        }
+        coffs.push_back(ev.begin);
+        known.push_back(ev.known);
+        hashes.insert(hashes.end(), ev.hash, ev.hash + 32);
+        who.emplace_back(i, e);
+        at = ev.end;
+      }
+      ws[i]->refs.resize(ws[i]->cf.events.size());
+    }
+    coffs.push_back(at);
+    const uint32_t nrec = (uint32_t)who.size();
+    std::vector<pfscdc_ref> refs(nrec);
+    if (nrec)
+      rc = create_refs_device(ctx, d, total, coffs.data(), nrec, hashes.data(), known.data(),
+                              refs.data(), dct);
+    for (uint32_t r = 0; r < nrec && !rc; r++) {
+      if (who[r].first == SIZE_MAX) continue;
+      pfscdc_writer* w = ws[who[r].first];
+      w->refs[who[r].second] = refs[r];
+      if (up) rc = upload(w->store, refs[r], dct, coffs[r], coffs[r + 1]);
+    }
+  }
+  const auto t4 = now();
+  if (d) (void)hipFree(d);
+  if (dct) (void)hipFree(dct);
+  for (size_t i = 0; i < n; i++) {
+    pfscdc_writer* w = ws[i];
+    w->closed = true;
+    w->files.clear();
+    w->buf.clear();
+    w->buf.shrink_to_fit();
+    w->spans.clear();
+    w->span_bytes = 0;
+    if (rc) {
+      w->cf.events.clear();
+      w->cf.outs.clear();
+      set_err(w, rc);
+      continue;
+    }
+    int r2 = callbacks(w);
+    if (r2 && !rc) rc = r2;
+  }
+  if (trace)
+    fprintf(stderr, "[pfscdc] close_group n=%zu bytes=%lu upload %.1f ms scan %.1f replay %.1f "
+            "create %.1f callbacks %.1f\n", n, (unsigned long)total, ms(t0, t1), ms(t1, t2),
+            ms(t2, t3), ms(t3, t4), ms(t4, now()));
+  return rc;
+}
+
+// Write of n caller-owned bytes kept until the writer flushes (no copy).
+int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n) {
+  if (w->err) return w->err;
+  if (w->closed || w->buffering || w->files.empty())
+    return pfscdc_writer_write(w, p, n);  // anything unusual: the copying path
+  if (n) {
+    w->spans.emplace_back(p, n);
+    w->span_bytes += n;
+  }
+  return PFSCDC_OK;
+}
+
+}  // namespace pfscdc
 
 extern "C" {
 

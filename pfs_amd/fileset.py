@@ -22,6 +22,8 @@ import ctypes as C
 from dataclasses import dataclass
 from typing import Optional
 
+import numpy as np
+
 from . import _lib
 from .cdc import ChunkParams, Chunker
 
@@ -101,9 +103,10 @@ class UnorderedWriter:
             raise _lib.PfsCdcError(rc, f"{what}: {msg.decode() if msg else ''}")
 
     def put(self, p: str, tag: str, append_file: bool, data) -> None:
-        buf = bytes(data)
+        arr = np.frombuffer(data, dtype=np.uint8)  # no copy: the library copies once
         self._check(self.lib.pfscdc_uw_put(self._w, p.encode(), tag.encode(), int(append_file),
-                                           buf, len(buf)), "Put")
+                                           arr.ctypes.data if arr.size else None, arr.size),
+                    "Put")
 
     def delete(self, p: str, tag: str = "") -> None:
         self._check(self.lib.pfscdc_uw_delete(self._w, p.encode(), tag.encode()), "Delete")
