@@ -1,7 +1,7 @@
 # Builds the product library (gfx950) and the oracle/CPU-baseline library.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -pthread
 SRC := pfs_amd/csrc/cdc_kernels.hip pfs_amd/csrc/pfscdc.cpp pfs_amd/csrc/writer.cpp pfs_amd/csrc/fileset.cpp pfs_amd/csrc/gorand.cpp
 HDR := include/pfscdc.h pfs_amd/csrc/pfscdc_internal.h
 

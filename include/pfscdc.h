@@ -329,6 +329,9 @@ int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int appe
  * and the live files of the filesets this writer serialized; no parent fileset). */
 int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag);
 int pfscdc_uw_close(pfscdc_uwriter* w); /* serializes the rest (Close, :171-179) */
+/* Serialized filesets are written in groups of up to PFSCDC_UW_INFLIGHT bytes (env, default
+ * 8 GiB) on a background thread while Puts continue; the event callback may run on that
+ * thread (one group at a time, events in order).  Filesets are readable after Close. */
 uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w);
 /* Fileset i's Primitive (pointers valid until pfscdc_uw_destroy). */
 int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* out);

@@ -17,8 +17,10 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pfscdc_internal.h"
@@ -456,9 +458,37 @@ struct FilesetWriter {  // fileset/writer.go:21-182
 // the Buffer keeps each file as spans of it and the fileset's chunk writer uploads the spans
 // straight from here in path order.  Recycled through the writer's pool.
 struct Arena {
-  std::unique_ptr<uint8_t[]> p;
+  uint8_t* p = nullptr;
   uint64_t cap = 0, used = 0;
+  bool pinned = false;  // page-locked: the H2D upload runs at full PCIe rate
+  ~Arena() {
+    if (pinned) (void)hipHostFree(p);
+    else delete[] p;
+  }
 };
+
+// memcpy split over threads for large Puts (one core copies ~10 GB/s)
+void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  constexpr uint64_t kMin = 8ull << 20;
+  static const unsigned kThreads = [] {
+    const char* e = getenv("PFSCDC_COPY_THREADS");
+    const unsigned hw = std::thread::hardware_concurrency();
+    return e ? (unsigned)atoi(e) : std::min(8u, hw ? hw : 1u);
+  }();
+  const unsigned t = n < kMin || kThreads < 2 ? 1u : (unsigned)std::min<uint64_t>(kThreads, n / (kMin / 2));
+  if (t <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t part = (n / t + 4095) & ~4095ULL;
+  for (unsigned i = 1; i < t; i++) {
+    const uint64_t a = std::min<uint64_t>(n, part * i), b = std::min<uint64_t>(n, part * (i + 1));
+    if (b > a) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min<uint64_t>(n, part));
+  for (auto& x : th) x.join();
+}
 
 struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFiles does
   std::map<std::string, std::map<std::string, std::vector<Span>>> additive;
@@ -496,6 +526,10 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   // serializing one at a time; each fileset's chunk stream is independent.
   std::vector<Buffer> pending;
   std::vector<std::unique_ptr<Arena>> pool;  // arenas of written filesets, for reuse
+  std::mutex pool_mu;
+  std::vector<Buffer> in_flight;             // the group the worker writes
+  std::thread worker;
+  int worker_rc = PFSCDC_OK;
   uint64_t pending_bytes = 0, inflight_bytes = 8ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
                         std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
@@ -509,6 +543,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   }
 
   std::unique_ptr<Arena> new_arena() {
+    std::lock_guard<std::mutex> lk(pool_mu);
     if (!pool.empty()) {
       std::unique_ptr<Arena> a = std::move(pool.back());
       pool.pop_back();
@@ -517,8 +552,12 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     }
     auto a = std::make_unique<Arena>();
     a->cap = (uint64_t)mem_threshold;  // a Buffer never holds more than memThreshold bytes
-    a->p.reset(new (std::nothrow) uint8_t[a->cap]);
-    if (!a->p) return nullptr;
+    if (hipHostMalloc((void**)&a->p, a->cap, hipHostMallocDefault) == hipSuccess) {
+      a->pinned = true;
+    } else {
+      a->p = new (std::nothrow) uint8_t[a->cap];
+      if (!a->p) return nullptr;
+    }
     return a;
   }
 
@@ -535,24 +574,24 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     buffer = Buffer();
     mem_available = mem_threshold;
     next_fileset++;
-    return pending_bytes >= inflight_bytes ? flush_pending() : PFSCDC_OK;
+    return pending_bytes >= inflight_bytes ? flush_pending(true) : PFSCDC_OK;
   }
 
-  int flush_pending() {  // fileset.Writer for each pending buffer, data streams together
-    if (pending.empty()) return PFSCDC_OK;
-    const uint32_t fs0 = next_fileset - (uint32_t)pending.size();
+  // Writes one group of serialized buffers: a fileset.Writer each, their data streams
+  // through one grouped close, then their indexes; the arenas go back to the pool.
+  int write_group(std::vector<Buffer>& group, uint32_t fs0) {
     std::vector<std::unique_ptr<FilesetWriter>> fws;
     std::vector<pfscdc_writer*> cws;
     int rc = PFSCDC_OK;
-    for (size_t i = 0; i < pending.size() && !rc; i++) {
+    for (size_t i = 0; i < group.size() && !rc; i++) {
       fws.push_back(std::make_unique<FilesetWriter>(&st, fs0 + (uint32_t)i));
       FilesetWriter& fw = *fws.back();
       rc = fw.open();
-      const uint8_t* base = pending[i].arena ? pending[i].arena->p.get() : nullptr;
-      for (auto& p : pending[i].additive)
+      const uint8_t* base = group[i].arena ? group[i].arena->p : nullptr;
+      for (auto& p : group[i].additive)
         for (auto& t : p.second)
           if (!rc) rc = fw.add(p.first, t.first, base, t.second);
-      for (auto& p : pending[i].deletive)
+      for (auto& p : group[i].deletive)
         for (auto& t : p.second)
           if (!rc) rc = fw.del(p.first, t);
       cws.push_back(fw.cw);
@@ -562,11 +601,30 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
       rc = fws[i]->finish();
       if (!rc) filesets.push_back(std::move(fws[i]->info));
     }
-    for (Buffer& b : pending)
+    fws.clear();
+    std::lock_guard<std::mutex> lk(pool_mu);
+    for (Buffer& b : group)
       if (b.arena) pool.push_back(std::move(b.arena));
-    pending.clear();
-    pending_bytes = 0;
     return rc;
+  }
+
+  int join() {  // waits for the group being written in the background
+    if (worker.joinable()) worker.join();
+    return worker_rc;
+  }
+
+  // Hands the pending buffers to a background thread (async) or writes them here; at most
+  // one group is in flight, so Puts keep filling arenas while the GPU writes the last group.
+  int flush_pending(bool async) {
+    int rc = join();
+    if (rc || pending.empty()) return rc;
+    const uint32_t fs0 = next_fileset - (uint32_t)pending.size();
+    in_flight.clear();
+    in_flight.swap(pending);
+    pending_bytes = 0;
+    if (!async) return write_group(in_flight, fs0);
+    worker = std::thread([this, fs0] { worker_rc = write_group(in_flight, fs0); });
+    return PFSCDC_OK;
   }
 
   int put(const std::string& p, std::string tag, bool append, const uint8_t* data, uint64_t n) {
@@ -580,7 +638,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
       if (got) {
         if (!buffer.arena && !(buffer.arena = new_arena())) return PFSCDC_ENOMEM;
         Arena& a = *buffer.arena;
-        std::memcpy(a.p.get() + a.used, data + pos, got);
+        copy_parallel(a.p + a.used, data + pos, got);
         if (!w->empty() && w->back().off + w->back().len == a.used) w->back().len += got;
         else w->push_back(Span{a.used, got});
         a.used += got;
@@ -664,7 +722,7 @@ int pfscdc_uw_close(pfscdc_uwriter* w) {
   if (w->closed) return PFSCDC_OK;
   w->closed = true;
   int rc = w->serialize();
-  if (!rc) rc = w->flush_pending();
+  if (!rc) rc = w->flush_pending(false);
   return rc ? w->fail(rc) : PFSCDC_OK;
 }
 
@@ -686,6 +744,7 @@ int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* 
 }
 
 int pfscdc_uw_destroy(pfscdc_uwriter* w) {
+  if (w) w->join();
   delete w;
   return PFSCDC_OK;
 }

@@ -88,7 +88,12 @@ def workload(seed, nfiles, max_len, dirs=4):
     return ops, data
 
 
-def test_unordered_writer_many_filesets_multilevel_index():
+@pytest.mark.parametrize("inflight", [None, "300000"])
+def test_unordered_writer_many_filesets_multilevel_index(inflight, monkeypatch):
+    # inflight: serialized filesets are written in groups of up to this many bytes (the
+    # default holds all of them until Close); the output must not depend on the grouping
+    if inflight:
+        monkeypatch.setenv("PFSCDC_UW_INFLIGHT", inflight)
     ops, _ = workload(1, 160, 40_000)
     ops.append(("delete", "/d1/", ""))
     ops.append(("put", "/d1/again", "", False, b"xyz" * 1000))
