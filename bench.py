@@ -329,11 +329,32 @@ def main():
         for _ in range(n_e2e):
             e2e_chunker.scan(hnp, boffs)
         te = (time.perf_counter() - t0) / n_e2e
-        out["e2e"] = {"value": round(sbytes / te / GIB, 3), "unit": "GiB/s",
-                      "ms_per_batch": round(te * 1e3, 3),
-                      "note": "one configs[1] batch from pinned host memory: hipMemcpyAsync "
-                              "H2D + kernels + records D2H, serial (no overlap)"}
-        e2e_chunker.close()
+        # pipelined: two contexts (two streams) alternate, so batch k+1's H2D copy runs
+        # while batch k hashes
+        pipe = [e2e_chunker, Chunker(params, device=local)]
+        pipe[1].scan(hnp, boffs)
+        n_pipe, busy = 8, [False, False]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_pipe):
+            k = i % 2
+            if busy[k]:
+                pipe[k].wait()
+            pipe[k].scan_async(hnp, boffs)
+            busy[k] = True
+        for k in range(2):
+            if busy[(n_pipe + k) % 2]:
+                pipe[(n_pipe + k) % 2].wait()
+        tp = (time.perf_counter() - t0) / n_pipe
+        out["e2e"] = {"value": round(sbytes / tp / GIB, 3), "unit": "GiB/s",
+                      "ms_per_batch": round(tp * 1e3, 3),
+                      "serial_value": round(sbytes / te / GIB, 3),
+                      "note": "configs[1] batches from pinned host memory (hipMemcpyAsync H2D + "
+                              "kernels + records D2H), two contexts on two streams alternating "
+                              "so each batch's copy overlaps the previous batch's kernels; "
+                              "serial_value: one batch at a time"}
+        for c in pipe:
+            c.close()
         del host
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
