@@ -192,7 +192,8 @@ def main():
         fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
         batches.append(t)
     chunker, data = chunkers[0], batches[0]
-    cap = pd.max_segments(sizes, params.min_chunk)
+    # all_gather_into_tensor needs equal blocks: the capacity of the largest shard
+    cap = max(pd.max_segments(workload(args, world, r)[0], params.min_chunk) for r in range(world))
     gather = world > 1 or args.config == "c5"
     torch.cuda.synchronize()
     acc = {"scan": 0.0, "compact": 0.0, "select": 0.0, "hash": 0.0, "total": 0.0}
