@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
                          "§8 next row 1) inside the step")
-    ap.add_argument("--path", default="put", choices=["put", "get", "commit", "uw"],
+    ap.add_argument("--path", default="put", choices=["put", "get", "commit", "uw", "rechunk"],
                     help="put: the ingest path (default); get: chunk.Get of the step's chunks "
                          "(verify BLAKE2b of the stored bytes against Ref.Id, ChaCha20 "
                          "decrypt), §8 next row 3, device-resident in and out; commit: the "
@@ -67,6 +67,8 @@ def parse():
                          "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk")
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
+    ap.add_argument("--rechunk-writers", type=int, default=10,
+                    help="rechunk: writers the file was written by (TestStableHash shape)")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
                     help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
@@ -229,6 +231,9 @@ def main():
     if args.path == "get":
         return bench_get(args, world, rank, local, dev, chunkers[0], batches[0], offs, total,
                          info, scaling, params, np, torch, dist)
+    if args.path == "rechunk":
+        return bench_rechunk(args, world, rank, dev, chunkers[0], batches[0], info, scaling,
+                             params, np, torch, dist)
     if args.path == "uw":
         return bench_uw(args, world, rank, dev, chunkers[0], batches[0], sizes, info, scaling,
                         params, np, torch, dist)
@@ -665,6 +670,65 @@ def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params
         "split_ms": {k: round(v / K, 1) for k, v in split.items()},
         "note": "put_ms: the Put loop (one host copy into the fileset arenas, serializations "
                 "deferred); close_ms: the grouped GPU write of every fileset plus the indexes",
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_rechunk(args, world, rank, dev, chunker, data, info, scaling, params, np, torch,
+                  dist):
+    """Re-chunk path (MergeFileReader.Hash, the Writer.Copy machinery): the step's first
+    1 GiB as one file written by --rechunk-writers writers (each its own chunk stream,
+    ciphertexts uploaded to the in-memory store), then the merged file's hash: Copy of every
+    DataRef through a fresh writer, whole aligned chunks passed through, the rest read back
+    (chunk.Get on the GPU) and re-rolled.  Checked against the single-writer hash."""
+    from pfs_amd import chunk as pc
+
+    nbytes = min(1 << 30, data.numel())
+    host = data[:nbytes].cpu().numpy()
+    chunker.close()
+    store = pc.ChunkStore()
+    st = pc.Storage(dev.index or 0, store=store)
+
+    def write(parts):
+        refs = []
+        w = st.new_writer("w", lambda anns: refs.extend(a.next_data_ref for a in anns
+                                                         if a.next_data_ref is not None))
+        for part in parts:
+            w.annotate(pc.Annotation(data=0))
+            w.write(part)
+        w.close()
+        return refs
+
+    single = write([host])  # the stable-hash reference: one writer
+    k = max(1, args.rechunk_writers)
+    size = (nbytes + k - 1) // k
+    refs = []
+    for off in range(0, nbytes, size):
+        refs += write([host[off:off + size]])
+    want = pc.hash_data_refs([d.hash for d in single], device=dev.index or 0)
+    for _ in range(args.warmup):
+        pc.merge_file_hash(store, refs, device=dev.index or 0)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = pc.merge_file_hash(store, refs, device=dev.index or 0)
+    elapsed = time.perf_counter() - t0
+    K = max(args.steps, 1)
+    edge = sum(1 for d in refs if d.ref.edge)
+    info.update({"path": "rechunk (MergeFileReader.Hash of a file written by %d writers)" % k,
+                 "file_bytes": nbytes, "data_refs": len(refs), "edge_data_refs": edge,
+                 "store_chunks": len(store)})
+    out = {
+        "metric": "GiB/s of file bytes through MergeFileReader.Hash (Writer.Copy re-chunking)",
+        "value": round(nbytes * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 bytes generated in HBM, copied to host)",
+        "config": info,
+        "parity": {"merged_hash_equals_single_writer_hash": got == want},
     }
     if rank == 0:
         print(json.dumps(out))

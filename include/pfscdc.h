@@ -255,6 +255,10 @@ int pfscdc_writer_set_store(pfscdc_writer* w, pfscdc_store* store, int upload);
  * boundary are buffered and passed through by reference (cheap copy, a callback with
  * chunk.copied = 1); anything else is read back and re-rolled like written bytes. */
 int pfscdc_writer_copy(pfscdc_writer* w, const pfscdc_full_dataref* dr);
+/* Optional hint before a run of Copies: verifies and decrypts, in one batch, every chunk
+ * those DataRefs will certainly be re-rolled from (edge chunks, DataRefs not starting at
+ * offset 0), so their BLAKE2b chains run in parallel instead of one per Copy. */
+int pfscdc_writer_prefetch(pfscdc_writer* w, const pfscdc_full_dataref* drs, uint32_t n);
 /* MergeFileReader.Hash (fileset/merge.go:125-143): a fresh writer on ctx (no upload), one
  * annotation, Copy of every DataRef, Close; out = BLAKE2b-256 over the resolved DataRefs'
  * hashes (hashDataRefs, fileset/util.go:149-158). */

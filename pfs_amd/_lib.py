@@ -41,7 +41,7 @@ EXPORTED = [
     "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_path_clean",
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
-    "pfscdc_merge_file_hash", "pfscdc_last_create_timings",
+    "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
 ]
 
 
@@ -206,6 +206,7 @@ def load() -> C.CDLL:
             "pfscdc_store_count": (u64, [vp]),
             "pfscdc_writer_set_store": (i32, [vp, vp, i32]),
             "pfscdc_writer_copy": (i32, [vp, P(FullDataRef)]),
+            "pfscdc_writer_prefetch": (i32, [vp, P(FullDataRef), u32]),
             "pfscdc_merge_file_hash": (i32, [vp, vp, P(FullDataRef), u32, vp]),
         }
         for name, (res, args) in sig.items():

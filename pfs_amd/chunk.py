@@ -228,6 +228,13 @@ class Writer:
         self._check(self.lib.pfscdc_writer_write(self._w, buf, len(buf)), "Write")
         return len(buf)
 
+    def prefetch(self, data_refs: list) -> None:
+        """Batch chunk.Get of the chunks these DataRefs will certainly be re-rolled from."""
+        arr = (_lib.FullDataRef * max(1, len(data_refs)))()
+        for i, d in enumerate(data_refs):
+            arr[i] = _full(d)
+        self._check(self.lib.pfscdc_writer_prefetch(self._w, arr, len(data_refs)), "prefetch")
+
     def copy(self, data_ref: DataRef) -> None:
         """Writer.Copy (writer.go:315-420)."""
         f = _full(data_ref)

@@ -21,6 +21,7 @@
 // last open annotation (bytes written after a flush that stopped at a cut).  A flush scans
 // them and replays the segments; a PARTIAL flush (Copy needs buf.Len()) withholds the last
 // annotation's bytes after its last cut, which stay pending as a continuation.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -159,6 +160,7 @@ struct pfscdc_writer {
   std::vector<uint8_t> hashes, known;
   std::vector<pfscdc_ref> refs;
   std::vector<uint8_t> fetched;       // scratch: a chunk read back for Copy
+  std::map<std::string, std::string> plain;  // chunks verified + decrypted ahead (prefetch)
   uint8_t* d_buf = nullptr;           // ref_ids: carry ++ pending files on the device
   uint8_t* d_ctext = nullptr;         // upload: ciphertexts, same layout as d_buf
   uint64_t d_cap = 0;
@@ -358,6 +360,14 @@ int append_bytes(pfscdc_writer* w, const uint8_t* p, uint64_t n) {
 // DataReader.Get (reader.go) via chunk.Get on the GPU, then roll (flushDataRef, :394-401).
 int flush_data_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {
   if (!w->store) return set_err(w, PFSCDC_ESTATE);
+  auto pc = w->plain.find(std::string((const char*)dr.ref.id, 32));
+  if (pc != w->plain.end()) {
+    if (dr.data.offset_bytes < 0 || dr.data.size_bytes < 0 ||
+        (uint64_t)(dr.data.offset_bytes + dr.data.size_bytes) > pc->second.size())
+      return set_err(w, PFSCDC_EINVAL);
+    return append_bytes(w, (const uint8_t*)pc->second.data() + dr.data.offset_bytes,
+                        (uint64_t)dr.data.size_bytes);
+  }
   auto it = w->store->objects.find(std::string((const char*)dr.ref.id, 32));
   if (it == w->store->objects.end()) return set_err(w, PFSCDC_ENOTFOUND);
   const std::string& ct = it->second;
@@ -692,6 +702,39 @@ int pfscdc_writer_write(pfscdc_writer* w, const void* data, uint64_t n) {
   return append_bytes(w, (const uint8_t*)data, n);
 }
 
+int pfscdc_writer_prefetch(pfscdc_writer* w, const pfscdc_full_dataref* drs, uint32_t n) {
+  // chunk.Get of every chunk these DataRefs will certainly be re-rolled from (edge chunks and
+  // DataRefs not starting at a chunk's first byte: maybeBufferDataRef never buffers them), in
+  // one batch: their BLAKE2b verifications run as parallel chains instead of one by one
+  if (!w || (n && !drs)) return PFSCDC_EINVAL;
+  if (w->err) return w->err;
+  if (!w->store) return PFSCDC_OK;
+  std::vector<std::string> ids;
+  std::vector<pfscdc_ref> refs;
+  std::vector<uint64_t> offs{0};
+  std::string ct;
+  for (uint32_t i = 0; i < n; i++) {
+    const pfscdc_full_dataref& d = drs[i];
+    if (!d.edge && d.data.offset_bytes == 0) continue;
+    std::string id((const char*)d.ref.id, 32);
+    if (w->plain.count(id) || std::find(ids.begin(), ids.end(), id) != ids.end()) continue;
+    auto it = w->store->objects.find(id);
+    if (it == w->store->objects.end()) continue;  // reported by the Copy that needs it
+    ids.push_back(id);
+    refs.push_back(d.ref);
+    ct += it->second;
+    offs.push_back(ct.size());
+  }
+  if (ids.empty()) return PFSCDC_OK;
+  std::vector<uint8_t> pt(ct.size() + 1), ok(ids.size());
+  int rc = pfscdc_get_chunks(w->ctx, ct.data(), ct.size(), 0, offs.data(), (uint32_t)ids.size(),
+                             refs.data(), pt.data(), 0, ok.data());
+  if (rc) return set_err(w, rc);
+  for (size_t i = 0; i < ids.size(); i++)  // a chunk failing verification stays uncached
+    if (ok[i]) w->plain.emplace(ids[i], std::string((const char*)pt.data() + offs[i], offs[i + 1] - offs[i]));
+  return PFSCDC_OK;
+}
+
 int pfscdc_writer_copy(pfscdc_writer* w, const pfscdc_full_dataref* dr) {
   if (!w || !dr) return PFSCDC_EINVAL;
   if (w->err) return w->err;
@@ -766,7 +809,8 @@ int pfscdc_merge_file_hash(pfscdc_ctx* ctx, pfscdc_store* store, const pfscdc_fu
   // WithNoUpload: the new chunks' ids never reach the result, so no Ref pass is run
   pfscdc_writer* w = new_writer(ctx, cb, &resolved, 0, false);
   w->store = store;
-  int rc = pfscdc_writer_annotate(w, 0);
+  int rc = pfscdc_writer_prefetch(w, drs, n);
+  if (!rc) rc = pfscdc_writer_annotate(w, 0);
   for (uint32_t i = 0; i < n && !rc; i++) rc = pfscdc_writer_copy(w, &drs[i]);
   if (!rc) rc = pfscdc_writer_close(w);
   pfscdc_writer_destroy(w);

@@ -130,3 +130,15 @@ def test_writer_errors_are_sticky():
     w.close()
     with pytest.raises(_lib.PfsCdcError):
         w.put("/y", "", False, b"abc")
+
+
+def test_reference_index_params_many_small_files_multilevel():
+    # ~6,000 small files: ~1.3 MB of level-0 index entries, so the reference's own index
+    # chunking (avgBits 20, 1 MB / 20 MB, seed = level) cuts level 0 and builds level 1
+    data = synthetic_bytes([0, 6000 * 97], 13).tobytes()
+    ops = [("put", f"/dir{i % 7}/file-{i:06d}", "", False, data[i * 97:(i + 1) * 97])
+           for i in range(6000)]
+    want, got, wlog, glog = run_both(ops, Ch.Params(), 10 ** 9)
+    levels = {e[2] for e in wlog[0] if e[0] == "chunk" and e[1] == 0}
+    assert max(levels) >= 1, levels
+    check(want, got, wlog, glog)
