@@ -342,11 +342,11 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                                 c->d_segs.p, c->d_seg_begin.p, st));
   }
   HIP_OK(c, hipEventRecord(c->ev[3], st));
-  if (nfiles)
+  if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
-  c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0;
+  c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p,
@@ -663,6 +663,50 @@ int scan_sync(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_de
   int rc = scan_async_impl(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles, options);
   if (rc) return rc;
   return pfscdc_wait(c);
+}
+
+// BLAKE2b-256 of n byte ranges [begins[i], begins[i] + sizes[i]) of a device buffer (one
+// record each, LPT order), into out (32 B per range).  Synchronous.
+int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
+                        const uint64_t* begins, const uint64_t* sizes, uint32_t n, uint8_t* out) {
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "hash during a pending scan");
+  if (n == 0) return PFSCDC_OK;
+  c->scan_valid = false;
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  HIP_OK(c, c->h_offs.ensure(n + 1));
+  HIP_OK(c, c->h_segs.ensure(n));
+  HIP_OK(c, c->h_seg_begin.ensure(1));
+  for (uint32_t i = 0; i < n; i++) {
+    c->h_offs.p[i] = begins[i];
+    pfscdc_segment& sg = c->h_segs.p[i];
+    std::memset(&sg, 0, sizeof sg);
+    sg.size = sizes[i];
+    sg.file = i;
+    sg.flags = PFSCDC_SEG_VALID;
+  }
+  c->h_offs.p[n] = nbytes;
+  c->h_seg_begin.p[0] = n;
+  HIP_OK(c, c->d_offs.ensure(n + 1));
+  HIP_OK(c, c->d_segs.ensure(n));
+  HIP_OK(c, c->d_order.ensure(n));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (n + 1),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * n,
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+  HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, n, c->d_order.p,
+                           c->d_qctr.p, c->num_cus, nbytes, st));
+  HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
+                           hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  for (uint32_t i = 0; i < n; i++) std::memcpy(out + 32ull * i, c->h_segs.p[i].hash, 32);
+  c->nsegs = 0;
+  c->have_refs = false;
+  return PFSCDC_OK;
 }
 
 // chunk.Create(ctx, CreateOptions{}, chunk, createFunc) for n chunks of a device buffer

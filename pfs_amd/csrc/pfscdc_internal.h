@@ -46,6 +46,11 @@ void generate_hashes(int64_t seed, uint64_t out[256]);
 const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
 void go_int63(int64_t seed, int64_t* out, int n);
 
+// internal scan option: cut positions only (segment records without their BLAKE2b)
+constexpr uint32_t kScanNoHash = 0x100;
+// BLAKE2b-256 of n ranges [begins[i], begins[i] + sizes[i]) of device data, into out
+int hash_records_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
+                        const uint64_t* begins, const uint64_t* sizes, uint32_t n, uint8_t* out);
 // pfscdc_scan with explicit options (the writer scans without per-segment refs).
 int scan_sync(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
               const uint64_t* file_offsets, uint32_t nfiles, uint32_t options);

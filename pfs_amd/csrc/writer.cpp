@@ -46,6 +46,8 @@ struct OpenAnnotation {
   uint8_t hash[32];  // hash of the (single) piece this annotation has in the open chunk
   bool has_next;     // a buffered (Copy) DataRef: Annotation.NextDataRef while buffering
   pfscdc_full_dataref next;
+  uint64_t pbegin = 0;    // buffer position of the piece
+  bool hpending = false;  // the piece's hash is still to be computed (deferred flush)
 };
 
 // One createChunk: the chunk's Ref fields, its annotations (outs[ann_begin, ann_end)) and
@@ -68,6 +70,8 @@ struct ChunkFormer {
   uint64_t pos = 0, open_start = 0;  // byte positions in the current buffer
   std::vector<ChunkEvent> events;
   std::vector<pfscdc_annotation_out> outs;
+  std::vector<uint64_t> out_begin;   // per out: buffer position of its piece
+  std::vector<uint8_t> out_pending;  // per out: piece hash still to be computed
 
   void reset_stream() {  // a fresh chunk.Writer
     annotations.clear();
@@ -89,6 +93,8 @@ struct ChunkFormer {
     for (const OpenAnnotation& a : annotations) {
       pfscdc_annotation_out o{};
       o.user = a.user;
+      out_begin.push_back(a.pbegin);
+      out_pending.push_back(a.size > 0 && a.hpending);
       if (a.size > 0) {
         o.has_data_ref = 1;
         std::memcpy(o.data_ref.hash, a.hash, 32);
@@ -108,7 +114,7 @@ struct ChunkFormer {
     events.push_back(ev);
     const uint64_t last_user = annotations.back().user;
     annotations.clear();
-    annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}});
+    annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}, pos, false});
     first = false;
     open_len = 0;
     open_start = pos;
@@ -117,13 +123,16 @@ struct ChunkFormer {
 
   void annotate(uint64_t user) {  // writer.go:118-130
     if (open_len >= avg && !annotations.empty()) create(false);
-    annotations.push_back(OpenAnnotation{user, 0, {}, false, {}});
+    annotations.push_back(OpenAnnotation{user, 0, {}, false, {}, pos, false});
   }
 
-  void piece(const pfscdc_segment& s) {  // writeData (+ createChunk at a cut)
+  // writeData (+ createChunk at a cut); pending: the segment's hash was not computed yet
+  void piece(const pfscdc_segment& s, bool pending = false) {
     OpenAnnotation& a = annotations.back();
+    if (a.size == 0) a.pbegin = pos;
     a.size += (int64_t)s.size;
-    std::memcpy(a.hash, s.hash, 32);
+    if (!pending) std::memcpy(a.hash, s.hash, 32);
+    a.hpending = pending;
     open_len += (int64_t)s.size;
     pos += s.size;
     if (s.flags & PFSCDC_SEG_CUT) create(false);
@@ -165,6 +174,10 @@ struct pfscdc_writer {
   uint8_t* d_ctext = nullptr;         // upload: ciphertexts, same layout as d_buf
   uint64_t d_cap = 0;
   ChunkFormer cf;
+  // deferred flushes (Copy's buf.Len() probes): buf[0, replayed) was replayed without its
+  // BLAKE2b; buf, carry and the formed chunks stay until a dispatching flush hashes them
+  uint64_t replayed = 0;
+  uint64_t dev_upto = 0;              // while deferring: buf[0, dev_upto) is already on the device
   bool buffering = false;             // Writer.buffering (Copy)
   bool closed = false;
   int64_t annotation_count = 0;
@@ -180,20 +193,36 @@ int set_err(pfscdc_writer* w, int code) {
   return w->err;
 }
 
-int ensure_device(pfscdc_writer* w, uint64_t need) {
+// Grows the device buffer to need bytes, keeping its first keep bytes.
+int ensure_device(pfscdc_writer* w, uint64_t need, uint64_t keep = 0) {
   if (need <= w->d_cap) return PFSCDC_OK;
+  const uint64_t want = need + need / 4;
+  uint8_t *nb = nullptr, *nc = nullptr;
+  if (hipSetDevice(pfscdc::ctx_device(w->ctx)) != hipSuccess ||
+      hipMalloc((void**)&nb, want) != hipSuccess)
+    return PFSCDC_ENOMEM;
+  if (w->upload && w->store && hipMalloc((void**)&nc, want) != hipSuccess) {
+    (void)hipFree(nb);
+    return PFSCDC_ENOMEM;
+  }
+  if (keep && w->d_buf && hipMemcpy(nb, w->d_buf, keep, hipMemcpyDeviceToDevice) != hipSuccess) {
+    (void)hipFree(nb);
+    if (nc) (void)hipFree(nc);
+    return PFSCDC_EHIP;
+  }
   if (w->d_buf) (void)hipFree(w->d_buf);
   if (w->d_ctext) (void)hipFree(w->d_ctext);
-  w->d_buf = w->d_ctext = nullptr;
-  w->d_cap = 0;
-  const uint64_t want = need + need / 4;
-  if (hipSetDevice(pfscdc::ctx_device(w->ctx)) != hipSuccess ||
-      hipMalloc((void**)&w->d_buf, want) != hipSuccess)
-    return PFSCDC_ENOMEM;
-  if (w->upload && w->store && hipMalloc((void**)&w->d_ctext, want) != hipSuccess)
-    return PFSCDC_ENOMEM;
+  w->d_buf = nb;
+  w->d_ctext = nc;
   w->d_cap = want;
   return PFSCDC_OK;
+}
+
+void clear_events(ChunkFormer& cf) {
+  cf.events.clear();
+  cf.outs.clear();
+  cf.out_begin.clear();
+  cf.out_pending.clear();
 }
 
 // The callbacks of the chunks formed in this flush, serially in chunk order (refs in w->refs).
@@ -202,7 +231,7 @@ int callbacks(pfscdc_writer* w) {
   int rc = PFSCDC_OK;
   for (size_t i = 0; i < cf.events.size() && !rc; i++) {
     ChunkEvent& ev = cf.events[i];
-    if (w->ref_ids) {
+    if (w->ref_ids && !ev.ref.copied) {
       ev.ref.has_ref = 1;
       ev.ref.ref = w->refs[i];
     }
@@ -210,8 +239,7 @@ int callbacks(pfscdc_writer* w) {
                        (uint32_t)(ev.ann_end - ev.ann_begin)) != 0)
       rc = set_err(w, PFSCDC_ECALLBACK);
   }
-  cf.events.clear();
-  cf.outs.clear();
+  clear_events(cf);
   return rc;
 }
 
@@ -233,30 +261,79 @@ int dispatch(pfscdc_writer* w, uint64_t valid) {
   ChunkFormer& cf = w->cf;
   const size_t n = cf.events.size();
   int rc = PFSCDC_OK;
+  w->refs.resize(n);
   if (w->ref_ids && n) {
-    w->chunk_offs.resize(n + 1);
-    w->hashes.resize(32 * n);
-    w->known.resize(n);
-    w->refs.resize(n);
-    for (size_t i = 0; i < n; i++) {
-      const ChunkEvent& ev = cf.events[i];
-      w->chunk_offs[i] = ev.begin;
-      w->known[i] = ev.known;
-      std::memcpy(&w->hashes[32 * i], ev.hash, 32);
+    std::vector<size_t> which;  // new chunks (cheap copies reference existing ones)
+    for (size_t i = 0; i < n; i++)
+      if (!cf.events[i].ref.copied) which.push_back(i);
+    const size_t m = which.size();
+    w->chunk_offs.resize(m + 1);
+    w->hashes.resize(32 * m);
+    w->known.resize(m);
+    std::vector<pfscdc_ref> refs(m);
+    for (size_t k = 0; k < m; k++) {
+      const ChunkEvent& ev = cf.events[which[k]];
+      w->chunk_offs[k] = ev.begin;
+      w->known[k] = ev.known;
+      std::memcpy(&w->hashes[32 * k], ev.hash, 32);
     }
-    w->chunk_offs[n] = cf.events[n - 1].end;
+    if (m) w->chunk_offs[m] = cf.events[which[m - 1]].end;
     uint8_t* ct = w->upload && w->store ? w->d_ctext : nullptr;
-    rc = pfscdc::create_refs_device(w->ctx, w->d_buf, valid, w->chunk_offs.data(), (uint32_t)n,
-                                    w->hashes.data(), w->known.data(), w->refs.data(), ct);
-    for (size_t i = 0; i < n && !rc && ct; i++)
-      rc = upload(w->store, w->refs[i], ct, cf.events[i].begin, cf.events[i].end);
+    if (m)
+      rc = pfscdc::create_refs_device(w->ctx, w->d_buf, valid, w->chunk_offs.data(),
+                                      (uint32_t)m, w->hashes.data(), w->known.data(),
+                                      refs.data(), ct);
+    for (size_t k = 0; k < m && !rc; k++) {
+      w->refs[which[k]] = refs[k];
+      if (ct) rc = upload(w->store, refs[k], ct, w->chunk_offs[k], w->chunk_offs[k + 1]);
+    }
     if (rc) {
-      cf.events.clear();
-      cf.outs.clear();
+      clear_events(cf);
       return set_err(w, rc);
     }
   }
   return callbacks(w);
+}
+
+// The piece hashes deferred by kPartial flushes (formed chunks' pieces and the open
+// chunk's), in one launch over the device buffer: the re-rolled chains run in parallel.
+int resolve_pending(pfscdc_writer* w, uint64_t valid) {
+  ChunkFormer& cf = w->cf;
+  std::vector<uint64_t> begins, sizes;
+  std::vector<std::pair<int, size_t>> who;  // (0: out, 1: open annotation), index
+  for (size_t i = 0; i < cf.outs.size(); i++)
+    if (cf.out_pending[i]) {
+      begins.push_back(cf.out_begin[i]);
+      sizes.push_back((uint64_t)cf.outs[i].data_ref.size_bytes);
+      who.emplace_back(0, i);
+    }
+  for (size_t i = 0; i < cf.annotations.size(); i++)
+    if (cf.annotations[i].hpending && cf.annotations[i].size > 0) {
+      begins.push_back(cf.annotations[i].pbegin);
+      sizes.push_back((uint64_t)cf.annotations[i].size);
+      who.emplace_back(1, i);
+    }
+  if (who.empty()) return PFSCDC_OK;
+  std::vector<uint8_t> h(32 * who.size());
+  int rc = pfscdc::hash_records_device(w->ctx, w->d_buf, valid, begins.data(), sizes.data(),
+                                       (uint32_t)who.size(), h.data());
+  if (rc) return set_err(w, rc);
+  for (size_t k = 0; k < who.size(); k++) {
+    const uint8_t* hk = h.data() + 32 * k;
+    if (who[k].first == 0) {
+      std::memcpy(cf.outs[who[k].second].data_ref.hash, hk, 32);
+      cf.out_pending[who[k].second] = 0;
+    } else {
+      OpenAnnotation& a = cf.annotations[who[k].second];
+      std::memcpy(a.hash, hk, 32);
+      a.hpending = false;
+    }
+  }
+  for (ChunkEvent& ev : cf.events)  // a one-DataRef chunk's hash is its piece's
+    if (!ev.ref.copied && ev.known)
+      for (size_t i = ev.ann_begin; i < ev.ann_end; i++)
+        if (cf.outs[i].has_data_ref) std::memcpy(ev.hash, cf.outs[i].data_ref.hash, 32);
+  return PFSCDC_OK;
 }
 
 // Runs the pending files through the GPU and replays the chunk state machine over their
@@ -277,65 +354,82 @@ int flush(pfscdc_writer* w, FlushMode mode) {
   if (nfiles == 0 && mode != kFinal) return PFSCDC_OK;
   ChunkFormer& cf = w->cf;
   const uint64_t nbytes = w->buf.size();
-  uint64_t base = 0;  // device position of the first pending byte
-  if (w->ref_ids) {
-    // [carry | files] contiguous on the device, files 16-byte aligned for the scan
-    const uint64_t cl = w->carry.size();
-    base = (cl + 15) & ~15ULL;
-    int rc = ensure_device(w, base + nbytes + 64);
-    if (rc) return set_err(w, rc);
-    if ((cl && hipMemcpy(w->d_buf + base - cl, w->carry.data(), cl, hipMemcpyHostToDevice) != hipSuccess) ||
-        (nbytes && hipMemcpy(w->d_buf + base, w->buf.data(), nbytes, hipMemcpyHostToDevice) != hipSuccess))
-      return set_err(w, PFSCDC_EHIP);
-    cf.open_start = base - cl;
-  } else {
-    cf.open_start = 0;
-  }
-  cf.pos = base;
-  uint64_t consumed = nbytes;  // pending bytes replayed
+  const uint64_t R = w->replayed;
+  // a kPartial flush defers the hashing unless the kept bytes have grown to a batch
+  const bool defer = mode == kPartial && nbytes < w->batch_bytes;
+  // [carry | buf] contiguous on the device (carry: the open chunk's bytes of earlier
+  // dispatched flushes, kept for chunk.Create)
+  const uint64_t cl = w->carry.size();
+  const uint64_t base = (cl + 15) & ~15ULL;
+  // while deferring, carry and buf[0, dev_upto) are already on the device: send the rest
+  const uint64_t have = R ? w->dev_upto : 0;
+  int rc = ensure_device(w, base + nbytes + 64, have ? base + have : 0);
+  if (rc) return set_err(w, rc);
+  if ((!have && cl && hipMemcpy(w->d_buf + base - cl, w->carry.data(), cl, hipMemcpyHostToDevice) != hipSuccess) ||
+      (nbytes > have && hipMemcpy(w->d_buf + base + have, w->buf.data() + have, nbytes - have,
+                                  hipMemcpyHostToDevice) != hipSuccess))
+    return set_err(w, PFSCDC_EHIP);
+  w->dev_upto = nbytes;
+  if (R == 0) cf.open_start = base - cl;  // else unchanged since the deferred flush
+  cf.pos = base + R;
+  uint64_t consumed = nbytes;  // bytes of buf replayed
   bool keep_tail = false;
   uint64_t tail_user = 0;
   if (nfiles) {
-    w->offsets.resize(nfiles + 1);
-    for (uint32_t f = 0; f < nfiles; f++) w->offsets[f] = w->files[f].begin;
-    w->offsets[nfiles] = nbytes;
-    int rc = w->ref_ids
-                 ? pfscdc::scan_sync(w->ctx, w->d_buf + base, nbytes, 1, w->offsets.data(), nfiles, 0)
-                 : pfscdc::scan_sync(w->ctx, w->buf.data(), nbytes, 0, w->offsets.data(), nfiles, 0);
+    // scan from a 16-byte aligned start; the few replayed bytes before base + R form a
+    // dummy file whose segments are ignored
+    const uint64_t start = (base + R) & ~15ULL;
+    const uint32_t dummy = start < base + w->files[0].begin ? 1 : 0;
+    w->offsets.clear();
+    if (dummy) w->offsets.push_back(0);
+    for (uint32_t f = 0; f < nfiles; f++) w->offsets.push_back(base + w->files[f].begin - start);
+    w->offsets.push_back(base + nbytes - start);
+    rc = pfscdc::scan_sync(w->ctx, w->d_buf + start, base + nbytes - start, 1, w->offsets.data(),
+                           nfiles + dummy, defer ? pfscdc::kScanNoHash : 0);
     if (rc) return set_err(w, rc);
     const pfscdc_segment* segs = pfscdc_segments(w->ctx);
     const uint64_t* begin = pfscdc_file_segment_begin(w->ctx);
     for (uint32_t f = 0; f < nfiles; f++) {
+      const uint32_t g = f + dummy;
       if (!w->files[f].cont) cf.annotate(w->files[f].user);
-      uint64_t end = begin[f + 1];
+      uint64_t end = begin[g + 1];
       if (mode == kPartial && f + 1 == nfiles) {
         // withhold the bytes after the last cut: the annotation is still being written
-        uint64_t s_end = begin[f];
-        for (uint64_t s = begin[f]; s < end; s++)
+        uint64_t s_end = begin[g];
+        for (uint64_t s = begin[g]; s < end; s++)
           if (segs[s].flags & PFSCDC_SEG_CUT) s_end = s + 1;
-        consumed = w->offsets[f] + (s_end > begin[f] ? segs[s_end - 1].offset + segs[s_end - 1].size : 0);
+        consumed = w->files[f].begin +
+                   (s_end > begin[g] ? segs[s_end - 1].offset + segs[s_end - 1].size : 0);
         keep_tail = consumed < nbytes;
         tail_user = w->files[f].user;
         end = s_end;
       }
-      for (uint64_t s = begin[f]; s < end; s++) cf.piece(segs[s]);
+      for (uint64_t s = begin[g]; s < end; s++) cf.piece(segs[s], defer);
     }
   }
   if (mode == kFinal) cf.close();
-  int rc = dispatch(w, base + nbytes);
+  w->files.clear();
+  if (defer) {  // everything stays: buf, carry, the formed chunks; only the tail is pending
+    w->replayed = consumed;
+    if (keep_tail) w->files.push_back(PendingFile{tail_user, consumed, true});
+    return PFSCDC_OK;
+  }
+  rc = resolve_pending(w, base + nbytes);
+  if (!rc) rc = dispatch(w, base + nbytes);
   if (rc) return rc;
-  if (w->ref_ids) {  // the open chunk's replayed bytes move to the front of the next flush
-    const uint64_t cl = w->carry.size();
+  {  // the open chunk's replayed bytes move to the front of the next flush
     const uint64_t keep_from = cf.open_start;  // >= base - cl
     const uint64_t keep_to = base + consumed;
     std::vector<uint8_t> next;
-    if (keep_from < base) next.assign(w->carry.begin() + (keep_from - (base - cl)), w->carry.end());
-    const uint64_t from_buf = keep_from > base ? keep_from - base : 0;
-    if (keep_to > base + from_buf)
-      next.insert(next.end(), w->buf.begin() + from_buf, w->buf.begin() + (keep_to - base));
+    if (w->ref_ids) {
+      if (keep_from < base) next.assign(w->carry.begin() + (keep_from - (base - cl)), w->carry.end());
+      const uint64_t from_buf = keep_from > base ? keep_from - base : 0;
+      if (keep_to > base + from_buf)
+        next.insert(next.end(), w->buf.begin() + from_buf, w->buf.begin() + (keep_to - base));
+    }
     w->carry.swap(next);
   }
-  w->files.clear();
+  w->replayed = 0;
   if (keep_tail) {
     w->buf.erase(w->buf.begin(), w->buf.begin() + consumed);
     w->files.push_back(PendingFile{tail_user, 0, true});
@@ -421,14 +515,16 @@ int maybe_cheap_copy(pfscdc_writer* w) {  // writer.go:403-420
   if (!la.has_next) return set_err(w, PFSCDC_ESTATE);  // Go: nil NextDataRef dereference
   const pfscdc_full_dataref& last = la.next;
   if (last.data.offset_bytes + last.data.size_bytes != last.ref_size) return PFSCDC_OK;
-  pfscdc_chunk_ref ref{};
-  ref.chunk_index = ~0ULL;
-  ref.size_bytes = last.ref_size;
-  ref.edge = last.edge;
-  ref.has_ref = 1;
-  ref.ref = last.ref;
-  ref.copied = 1;
-  std::vector<pfscdc_annotation_out> outs;
+  // the callback of a chunk that already exists: queued behind the chunks formed before it
+  const bool now = cf.events.empty();
+  ChunkEvent ev{};
+  ev.ref.chunk_index = ~0ULL;
+  ev.ref.size_bytes = last.ref_size;
+  ev.ref.edge = last.edge;
+  ev.ref.has_ref = 1;
+  ev.ref.ref = last.ref;
+  ev.ref.copied = 1;
+  ev.ann_begin = cf.outs.size();
   for (const OpenAnnotation& a : cf.annotations) {
     pfscdc_annotation_out o{};
     o.user = a.user;
@@ -436,15 +532,17 @@ int maybe_cheap_copy(pfscdc_writer* w) {  // writer.go:403-420
       o.has_data_ref = 1;
       o.data_ref = a.next.data;
     }
-    outs.push_back(o);
+    cf.outs.push_back(o);
+    cf.out_begin.push_back(0);
+    cf.out_pending.push_back(0);
   }
+  ev.ann_end = cf.outs.size();
+  cf.events.push_back(ev);
   const uint64_t last_user = la.user;
   cf.annotations.clear();  // splitAnnotations
-  cf.annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}});
+  cf.annotations.push_back(OpenAnnotation{last_user, 0, {}, false, {}, cf.pos, false});
   w->buffering = false;
-  if (w->cb && w->cb(w->user, &ref, outs.data(), (uint32_t)outs.size()) != 0)
-    return set_err(w, PFSCDC_ECALLBACK);
-  return PFSCDC_OK;
+  return now ? callbacks(w) : PFSCDC_OK;
 }
 
 int copy_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {  // writer.go:315-352
@@ -465,7 +563,7 @@ int copy_ref(pfscdc_writer* w, const pfscdc_full_dataref& dr) {  // writer.go:31
       int rc = flush(w, kPartial);
       if (rc) return rc;
     }
-    if (cf.open_len != 0 || !w->buf.empty()) return flush_data_ref(w, dr);
+    if (cf.open_len != 0 || w->buf.size() > w->replayed) return flush_data_ref(w, dr);
   } else {
     const pfscdc_full_dataref* prev = nullptr;  // getPrevDataRef
     for (auto it = cf.annotations.rbegin(); it != cf.annotations.rend() && !prev; ++it)
@@ -514,7 +612,8 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
   for (size_t i = 0; i < n && group; i++) {
     const pfscdc_writer* w = ws[i];
     group = !w->err && !w->closed && w->ctx == ctx && !w->buffering && w->carry.empty() &&
-            w->d_cap == 0 && w->ref_ids == ws[0]->ref_ids &&
+            w->d_cap == 0 && w->replayed == 0 && w->cf.events.empty() &&
+            w->ref_ids == ws[0]->ref_ids &&
             (w->upload && w->store) == (ws[0]->upload && ws[0]->store);
   }
   if (!group) {
