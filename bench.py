@@ -73,7 +73,8 @@ def parse():
                     help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="steps in flight (one GPU context + input buffer each)")
+                    help="steps in flight (one GPU context + input buffer each; --path commit: "
+                         "one context + host thread each over the step's one input buffer)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -189,7 +190,7 @@ def main():
     S = max(1, args.inflight)
     chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
     batches = []
-    for k in range(S):
+    for k in range(S if args.path != "commit" else 1):
         t = torch.empty(total, dtype=torch.uint8, device=dev)
         fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
         batches.append(t)
@@ -238,7 +239,7 @@ def main():
         return bench_uw(args, world, rank, dev, chunkers[0], batches[0], sizes, info, scaling,
                         params, np, torch, dist)
     if args.path == "commit":
-        return bench_commit(args, world, rank, dev, chunkers[0], batches[0], sizes, total, info,
+        return bench_commit(args, world, rank, dev, chunkers, batches[0], sizes, total, info,
                             scaling, params, np, torch, dist)
 
     run(args.warmup, False)
@@ -520,27 +521,38 @@ def commit_layout(sizes, mem_threshold):
     return pieces, streams
 
 
-def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scaling, params,
+def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, scaling, params,
                  np, torch, dist):
     """pachd data plane on the step's files: pieces / filesets (commit_layout), CDC + DataRef
     hashes (one scan of all pieces), chunk formation per fileset stream (pfscdc_form_chunks),
     chunk.Create of every formed chunk (pfscdc_create_refs: content hash of multi-DataRef
-    chunks, dek, ChaCha20 + BLAKE2b of the ciphertext)."""
+    chunks, dek, ChaCha20 + BLAKE2b of the ciphertext).
+
+    With --inflight S > 1, S contexts (S HIP streams) each run every S-th step from their own
+    host thread, so one step's chunk.Create tail (the serial BLAKE2b chains of its largest
+    chunks: content hash, then Ref.Id) overlaps the next step's scan and hashes.  The steps
+    read the same device buffer (the same files committed again; the library only reads it)."""
+    import threading
+
+    S = len(chunkers)
     pieces, streams = commit_layout(sizes, args.mem_threshold)
     poffs = np.zeros(len(pieces) + 1, dtype=np.uint64)
     poffs[1:] = np.cumsum(np.asarray(pieces, dtype=np.uint64))
     assert int(poffs[-1]) == total
-    chunker.set_ref_ids(False)
-    acc = {"scan": 0.0, "hash": 0.0, "total": 0.0, "create": 0.0, "create_content_hash": 0.0,
-           "create_ref_id": 0.0, "host_form_ms": 0.0}
-    last = {}
+    keys = ("scan", "hash", "total", "create", "create_content_hash", "create_ref_id",
+            "host_form_ms")
+    accs = [dict.fromkeys(keys, 0.0) for _ in range(S)]
+    lasts = [{} for _ in range(S)]
+    for ch in chunkers:
+        ch.set_ref_ids(False)
 
-    def step(record):
+    def step(k, record):
+        chunker, acc = chunkers[k], accs[k]
         res = chunker.scan(data, poffs)
         if record:
             t = chunker.timings()
-            for k in ("scan", "hash", "total"):
-                acc[k] += t[k]
+            for name in ("scan", "hash", "total"):
+                acc[name] += t[name]
         h0 = time.perf_counter()
         coffs, hashes, known = chunker.form_chunks(streams)
         if record:
@@ -551,16 +563,41 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
             ct = chunker.last_create_timings()
             acc["create_content_hash"] += ct["content_hash"]
             acc["create_ref_id"] += ct["ref_id"]
-        last.update(res=res, coffs=coffs, known=known, refs=refs)
+        lasts[k].update(res=res, coffs=coffs, known=known, refs=refs)
 
-    for _ in range(args.warmup):
-        step(False)
+    errors = []
+
+    def worker(k, nsteps, record):
+        try:
+            for _ in range(nsteps):
+                step(k, record)
+        except BaseException as e:  # re-raised on the main thread
+            errors.append(e)
+
+    def run(nsteps, record):
+        """nsteps steps, step i on context i % S; one host thread per context."""
+        counts = [len(range(k, nsteps, S)) for k in range(S)]
+        if S == 1:
+            worker(0, counts[0], record)
+        else:
+            ts = [threading.Thread(target=worker, args=(k, counts[k], record))
+                  for k in range(S) if counts[k]]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+        if errors:
+            raise errors[0]
+
+    for k in range(S):  # every context warms up (buffers sized) before the timed region
+        worker(k, max(args.warmup, 1) if S > 1 else args.warmup, False)
+    if errors:
+        raise errors[0]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    run(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -574,13 +611,15 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_step = int(bt.item())
     K = max(args.steps, 1)
-    avg = {k: v / K for k, v in acc.items()}
+    avg = {name: sum(a[name] for a in accs) / K for name in keys}
+    last = lasts[0]
     coffs, known = last["coffs"], last["known"]
     nch = len(coffs) - 1
     info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
                          "chunk.Create)", "mem_threshold": args.mem_threshold,
                  "filesets_per_step": len(streams) - 1, "pieces_per_step": len(pieces),
-                 "chunks_per_step": nch, "multi_dataref_chunks": int(nch - int(known.sum()))})
+                 "chunks_per_step": nch, "multi_dataref_chunks": int(nch - int(known.sum())),
+                 "steps_in_flight": S})
     ms = avg["create"]
     ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     out = {
@@ -591,19 +630,23 @@ def bench_commit(args, world, rank, dev, chunker, data, sizes, total, info, scal
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
-        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+        "kernel_ms": {name: round(v, 4) for name, v in avg.items()},
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
                      "kernel": "chunk.Create batch (content hash + dek + ChaCha20/BLAKE2b)"},
     }
+    if S > 1:
+        out["note"] = ("kernel_ms are per step on its own stream; with %d steps in flight they "
+                       "overlap, so ms_per_step < their sum" % S)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["parity"] = commit_parity(data, pieces, streams, poffs, last, params, np)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
-    chunker.close()
+    for ch in chunkers:
+        ch.close()
 
 
 def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params, np, torch,
