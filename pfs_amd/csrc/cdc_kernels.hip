@@ -79,6 +79,24 @@ PFS_DEV void load64(uint32_t (&w)[16], const uint8_t* p) {
   }
 }
 
+// Wave-uniform min / max of a 32-bit lane value (every lane active).
+PFS_DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = u < v ? u : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+PFS_DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = u > v ? u : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 PFS_DEV uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -910,7 +928,7 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 //   keystream is XORed into the LDS buffer and the plaintext stored to out.
 constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
 template <int MODE>
-__global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
+__global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
@@ -933,13 +951,21 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
   const uint32_t slot = (threadIdx.x >> 2) * kMsgStride;
   uint8_t* my = s_msg + slot + 32u * j;
 
-  // LDS addresses (buffer 0) of the 4 message words this lane consumes in each round
+  // Absolute LDS addresses (buffer 0) of the 4 message words this lane consumes in each
+  // round, 48 registers held for the whole kernel (the buffer parity is the ds_read offset
+  // immediate).  Left to itself the compiler keeps the sigma bytes packed and rebuilds each
+  // address with a v_add per read (48 VALU per block, ~8% of the hash); the empty asm makes
+  // the values opaque so they stay in registers (budget: amdgpu_waves_per_eu(1, 2)).
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)s_msg;
   uint32_t ma[12][4];
 #pragma unroll
   for (int r = 0; r < 12; r++) {
     const uint32_t pk = pick4(j, kSigmaPack[r][0], kSigmaPack[r][1], kSigmaPack[r][2], kSigmaPack[r][3]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) ma[r][k] = slot + ((pk >> (8 * k)) & 0xFFu);
+    for (int k = 0; k < 4; k++) {
+      ma[r][k] = lds_base + slot + ((pk >> (8 * k)) & 0xFFu);
+      asm volatile("" : "+v"(ma[r][k]));
+    }
   }
   // lane constants from immediates (v_cndmask), not loads: a load here would leave the
   // compiler unable to count vmcnt across the loop and it waits for vmcnt(0) every block
@@ -954,6 +980,11 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
                   (nseg > (uint64_t)gridDim.x * (kHashBlock / 4) ? 8192u : 0u);
   bool active = false;   // this quad holds a segment
   bool drained = false;  // wave-uniform: the queue is exhausted
+  // wave-uniform: blocks to come in which no quad can finish and the priority cannot change,
+  // so the refill ballot, the exit test and the priority ballot are skipped (they cost ~20
+  // VALU per block when evaluated every block)
+  uint32_t quiet = 0;
+  const bool graded = (prio_blocks & 0x40000000u) != 0;
   uint64_t L = 0, nblk = 0, blk = 0;
   const uint8_t* src = data;
   pfscdc_segment* seg = segs;
@@ -994,56 +1025,70 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
 
   auto step = [&](auto par) -> bool {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
-    if (!drained) {
-      const bool need = !active;
-      const uint64_t want = __ballot(need && j == 0);  // one bit per idle quad (its lane 0)
-      if (want) {
-        const uint32_t cnt = (uint32_t)__popcll(want);
-        const uint32_t leader = (uint32_t)__builtin_ctzll(want);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(counter, cnt);
-        base = (uint32_t)__shfl((int)base, (int)leader, 64);
-        if (need) {
-          const uint64_t below = want & ((1ULL << (lane & ~3u)) - 1);
-          const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(below);
-          if (idx < nseg) {
-            sidx = order[idx];
-            seg = segs + sidx;
-            L = seg->size;
-            if (CIPHER) {
-              const uint32_t* dk = reinterpret_cast<const uint32_t*>(refs[sidx].dek);
-              key_b = dk[j];
-              key_c = dk[4 + j];
+    if (quiet) {
+      quiet--;
+    } else {
+      if (!drained) {
+        const bool need = !active;
+        const uint64_t want = __ballot(need && j == 0);  // one bit per idle quad (its lane 0)
+        if (want) {
+          const uint32_t cnt = (uint32_t)__popcll(want);
+          const uint32_t leader = (uint32_t)__builtin_ctzll(want);
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(counter, cnt);
+          base = (uint32_t)__shfl((int)base, (int)leader, 64);
+          if (need) {
+            const uint64_t below = want & ((1ULL << (lane & ~3u)) - 1);
+            const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(below);
+            if (idx < nseg) {
+              sidx = order[idx];
+              seg = segs + sidx;
+              L = seg->size;
+              if (CIPHER) {
+                const uint32_t* dk = reinterpret_cast<const uint32_t*>(refs[sidx].dek);
+                key_b = dk[j];
+                key_c = dk[4 + j];
+              }
+              src = data + offs[seg->file] + seg->offset;
+              if (MODE != kModeHash && out) dst_base = out + offs[seg->file] + seg->offset;
+              nblk = L == 0 ? 1 : (L + 127) / 128;
+              blk = 0;
+              ha = h0a;
+              hb = h0b;
+              active = true;
+              load_block(0);
+              lds_put(cur);
+              if (nblk > 1) load_block(1);
             }
-            src = data + offs[seg->file] + seg->offset;
-            if (MODE != kModeHash && out) dst_base = out + offs[seg->file] + seg->offset;
-            nblk = L == 0 ? 1 : (L + 127) / 128;
-            blk = 0;
-            ha = h0a;
-            hb = h0b;
-            active = true;
-            load_block(0);
-            lds_put(cur);
-            if (nblk > 1) load_block(1);
           }
+          if ((uint64_t)base + cnt >= nseg) drained = true;
         }
-        if ((uint64_t)base + cnt >= nseg) drained = true;
       }
-    }
-    if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
-    if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
-      const uint64_t T = prio_blocks & 0x3fffffffu, rem = active ? nblk - blk : 0;
-      if (prio_blocks & 0x40000000u) {  // graded: 3 above 2T, 2 above T, 1 above T/2
-        if (__ballot(rem > 2 * T)) __builtin_amdgcn_s_setprio(3);
-        else if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
-        else if (__ballot(rem > T / 2)) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      } else {
-        if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
+      if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
+      if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
+        const uint64_t T = prio_blocks & 0x3fffffffu, rem = active ? nblk - blk : 0;
+        if (prio_blocks & 0x40000000u) {  // graded: 3 above 2T, 2 above T, 1 above T/2
+          if (__ballot(rem > 2 * T)) __builtin_amdgcn_s_setprio(3);
+          else if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
+          else if (__ballot(rem > T / 2)) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        } else {
+          if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
+          else __builtin_amdgcn_s_setprio(0);
+        }
       }
-    }
 
+      // next event: the step after the first active quad's last block, or the step at which
+      // the longest remaining chain drops to the priority threshold
+      const uint64_t rem64 = active ? nblk - blk : 0;
+      const uint32_t rem = rem64 > 0xffffffffULL ? 0xffffffffu : (uint32_t)rem64;
+      uint32_t q = wave_min_u32(active ? rem : 0xffffffffu) - 1;
+      if ((prio_blocks & 0x3fffffffu) && !graded) {
+        const uint32_t T = prio_blocks & 0x3fffffffu, rmax = wave_max_u32(rem);
+        if (rmax > T && rmax - T - 1 < q) q = rmax - T - 1;
+      }
+      quiet = graded ? 0u : q;
+    }
     const bool last = blk + 1 == nblk;
     if (MODE == kModeRefId) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1073,8 +1118,8 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint64_t x0 = lds_load<uint64_t>(s_msg + cur, ma[0][0]), x1 = lds_load<uint64_t>(s_msg + cur, ma[0][1]);
-    uint64_t x2 = lds_load<uint64_t>(s_msg + cur, ma[0][2]), x3 = lds_load<uint64_t>(s_msg + cur, ma[0][3]);
+    uint64_t x0 = lds_abs_u64(ma[0][0] + cur), x1 = lds_abs_u64(ma[0][1] + cur);
+    uint64_t x2 = lds_abs_u64(ma[0][2] + cur), x3 = lds_abs_u64(ma[0][3] + cur);
     const uint64_t t = last ? L : (blk + 1) * 128;
     uint64_t a = ha, b = hb, c = iv_c;
     uint64_t d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
@@ -1082,10 +1127,10 @@ __global__ __launch_bounds__(kHashBlock) void blake2b_kernel(
     for (int r = 0; r < 12; r++) {
       uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
       if (r < 11) {
-        y0 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][0]);
-        y1 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][1]);
-        y2 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][2]);
-        y3 = lds_load<uint64_t>(s_msg + cur, ma[r + 1][3]);
+        y0 = lds_abs_u64(ma[r + 1][0] + cur);
+        y1 = lds_abs_u64(ma[r + 1][1] + cur);
+        y2 = lds_abs_u64(ma[r + 1][2] + cur);
+        y3 = lds_abs_u64(ma[r + 1][3] + cur);
       }
 #ifdef PFS_HASH_CXX
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
