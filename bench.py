@@ -166,10 +166,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # PFS_BENCH_REHEARSE=1: rehearse the N>1 path with every rank on the box's device(s) and
+    # gloo (RCCL refuses two ranks on one GPU); the driver's scaling runs use RCCL.
+    rehearse = os.environ.get("PFS_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    cdev = torch.device("cpu") if rehearse else dev  # collectives' tensors
 
     params = ChunkParams()  # reference defaults: avgBits 23, seed 1, min 1 MB, max 20 MB
     sizes, fbase, seed, mode, info, scaling = workload(args, world, rank)
@@ -209,7 +218,7 @@ def main():
         res = chunkers[k].wait()
         pending[k] = False
         if gather:
-            last["index"] = pd.gather_index(res.segments, fbase, cap, device=dev) \
+            last["index"] = pd.gather_index(res.segments, fbase, cap, device=cdev) \
                 if world > 1 else local_index(res.segments, fbase)
         if record:
             for name, v in chunkers[k].timings().items():
@@ -255,10 +264,10 @@ def main():
     elapsed = time.perf_counter() - t0
     bytes_step = total
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        bt = torch.tensor([total], dtype=torch.float64, device=cdev)
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_step = int(bt.item())
 

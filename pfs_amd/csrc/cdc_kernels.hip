@@ -145,7 +145,7 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
                                           uint64_t h, uint64_t pos, uint64_t n,
                                           uint64_t tile_base, uint64_t mask64,
                                           const uint64_t* __restrict__ table,
-                                          uint32_t* s_count, uint32_t* s_cand) {
+                                          TileRec* __restrict__ rec) {
   const uint8_t* in = block_src(data, tail, n_main, pos);
   const uint8_t* out = pos >= 64 ? block_src(data, tail, n_main, pos - 64) : nullptr;
   for (int t = 0; t < 64; t++) {
@@ -154,8 +154,9 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
     const uint32_t bo = out ? out[t] : 0u;
     h = rotl1_64(h) ^ table[bi] ^ table[bo];
     if ((h & mask64) == 0 && i >= 63 && i < n) {
-      const uint32_t k = atomicAdd(s_count, 1u);
-      if (k < kTileCandCap) s_cand[k] = (uint32_t)(i - tile_base);
+      // unordered; compact_kernel sorts the tile's offsets (count > kTileK marks it dense)
+      const uint32_t k = atomicAdd(&rec->count, 1u);
+      if (k < (uint32_t)kTileK) rec->off[k] = (uint32_t)(i - tile_base);
     }
   }
 }
@@ -187,7 +188,7 @@ PFS_DEV uint64_t lds_read_async(uint32_t a) {
 }
 
 #ifndef PFS_EXP_AHEAD
-#define PFS_EXP_AHEAD 8
+#define PFS_EXP_AHEAD 6
 #endif
 static_assert(PFS_EXP_AHEAD >= 1 && 2 * (PFS_EXP_AHEAD - 1) <= 15, "lgkmcnt is 4 bits");
 constexpr int kRollAhead = PFS_EXP_AHEAD;
@@ -232,7 +233,7 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
     });                                                                                   \
     if (__builtin_expect(acc == 0, 0))                                                    \
       record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, (POS), n, tile_base,  \
-                   mask64, table, s_count, s_cand);                                       \
+                   mask64, table, rec);                                                   \
   }
 
 // --- narrow masks (average_bits <= 32): the rolling hash without the outgoing byte -----------
@@ -252,7 +253,7 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
 PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail,
                             uint64_t n_main, uint64_t pos, uint64_t n, uint64_t tile_base,
                             uint64_t mask64, const uint64_t* __restrict__ table,
-                            uint32_t* s_count, uint32_t* s_cand) {
+                            TileRec* __restrict__ rec) {
   uint64_t h = 0;
   if (pos >= 64) {
     const uint8_t* w = block_src(data, tail, n_main, pos - 64);
@@ -260,11 +261,11 @@ PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __r
   } else {
     for (int k = 0; k < 64; k++) h = rotl1_64(h) ^ table[0];
   }
-  record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, s_count, s_cand);
+  record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, rec);
 }
 
 #ifndef PFS_EXP_GAHEAD
-#define PFS_EXP_GAHEAD 12
+#define PFS_EXP_GAHEAD 10
 #endif
 static_assert(PFS_EXP_GAHEAD >= 1 && PFS_EXP_GAHEAD - 1 <= 15, "lgkmcnt is 4 bits");
 constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read_b64 each)
@@ -305,8 +306,7 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
       }                                                                                   \
     });                                                                                   \
     if (__builtin_expect(acc < cand_thr, 0))                                              \
-      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, s_count,     \
-                     s_cand);                                                             \
+      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec);        \
   }
 
 // Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
@@ -318,15 +318,13 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
 PFS_DEV uint32_t stage_swz(uint32_t r) { return (r >> 1) & 7u; }
 
 template <bool WIDE>
-__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void cdc_scan_kernel(
+__global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs) {
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
-  // images, then the tile's candidate count + list.
+  // images.  recs[] is zeroed before the launch; candidates are added to it directly.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* s_count = reinterpret_cast<uint32_t*>(smem + kScanCandLds);
-  uint32_t* s_cand = s_count + 4;
   const uint64_t n_main = n & ~63ULL;
 
   // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
@@ -349,10 +347,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2
     const uint32_t r = 8u * i + (lane >> 3);
     dma_off[i] = r * kStrip + 16u * ((lane & 7u) ^ stage_swz(r));
   }
+  __syncthreads();  // table copies written; from here on every wave runs on its own
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    if (threadIdx.x == 0) *s_count = 0;
-    __syncthreads();
+    TileRec* const rec = recs + tile;
     const uint64_t tile_base = tile * kTile;
     const uint64_t wave_base = tile_base + (uint64_t)wave * 64 * kStrip;
     if (wave_base < n) {  // wave-uniform
@@ -427,17 +425,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(2, 2
         }
       }
     }
-    __syncthreads();
-    const uint32_t cnt = *s_count;
-    TileRec* rec = recs + tile;
-    if (threadIdx.x == 0) rec->count = cnt;
-    if (cnt <= (uint32_t)kTileK && threadIdx.x < cnt) {
-      const uint32_t v = s_cand[threadIdx.x];
-      uint32_t rank = 0;
-      for (uint32_t u = 0; u < cnt; u++) rank += s_cand[u] < v;
-      rec->off[rank] = v;
-    }
-    __syncthreads();
   }
 }
 
@@ -491,7 +478,17 @@ __global__ __launch_bounds__(kCompactBlock) void compact_kernel(
     if (t < ntiles) {
       const uint64_t ts = t * kTile;
       if (c <= (uint32_t)kTileK) {
-        for (uint32_t i = 0; i < c; i++) entries[ex + i] = ts + recs[t].off[i];
+        // the scan records a tile's offsets in arrival order; place each by its rank
+        uint32_t o[kTileK];
+#pragma unroll
+        for (int i = 0; i < kTileK; i++) o[i] = i < (int)c ? recs[t].off[i] : ~0u;
+#pragma unroll
+        for (int i = 0; i < kTileK; i++) {
+          uint32_t rank = 0;
+#pragma unroll
+          for (int j = 0; j < kTileK; j++) rank += o[j] < o[i];
+          if (i < (int)c) entries[ex + rank] = ts + o[i];
+        }
       } else {
         const uint64_t te = (ts + kTile < n) ? ts + kTile : n;
         entries[ex] = kDenseBit | (te - 1);  // sorts as the tile's last byte

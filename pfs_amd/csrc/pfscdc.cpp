@@ -323,6 +323,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main,
                              hipMemcpyDeviceToDevice, st));
   HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
+  // the scan adds candidates to the tile records with atomics
+  if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
   if (c->ntiles) {

@@ -7,16 +7,20 @@
 
 namespace pfscdc {
 
-// candidate scan geometry: 512 lanes x 4 KiB strips = 2 MiB tile per workgroup iteration
-constexpr int kScanBlock = 512;  // 8 waves (2 per SIMD): 64 KiB table + 8 x 8 KiB staging
+// candidate scan geometry: waves x 64 lanes x 4 KiB strips per tile.  Candidates go
+// straight to the tile's record in global memory (zeroed before the scan), so waves never
+// synchronise per tile and all LDS beyond the table is staging.
+#ifndef PFS_SCAN_WAVES
+#define PFS_SCAN_WAVES 12
+#endif
+constexpr int kScanWaves = PFS_SCAN_WAVES;  // 12 = 3 per SIMD: LDS exactly full (8: 2 per SIMD, 3.5% slower)
+constexpr int kScanBlock = 64 * kScanWaves;
 constexpr int kStrip = 4096;
 constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
 constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
-constexpr int kTileCandCap = 64;    // LDS staging per tile
 constexpr uint32_t kTableLdsBytes = 256u * 256u;  // T x 32 bank-disjoint copies
 constexpr uint32_t kStageBytes = 64u * 128u;       // per-wave LDS-DMA image: 64 rows x 128 B
-constexpr uint32_t kScanCandLds = kTableLdsBytes + (kScanBlock / 64) * kStageBytes;
-constexpr uint32_t kScanLdsBytes = kScanCandLds + 16 + 4 * kTileCandCap;
+constexpr uint32_t kScanLdsBytes = kTableLdsBytes + kScanWaves * kStageBytes;
 static_assert(kScanLdsBytes <= 160 * 1024, "scan kernel LDS budget");
 constexpr int kCompactBlock = 1024;
 constexpr int kSelectBlock = 256;   // 4 files (waves) per block
