@@ -139,9 +139,12 @@ def test_index_writer_seed0_avgbits20():
         assert_same(chunker_for(p).scan(data, offs), data, offs, p)
 
 
-def test_candidate_list_matches_oracle():
-    # ~2 candidates per 2 MiB tile: every tile stays sparse (<= 15 stored candidates)
-    p = Ch.Params(average_bits=20, seed=1, min=2000, max=30000)
+@pytest.mark.parametrize("bits", [20, 19])
+def test_candidate_list_matches_oracle(bits):
+    # ~3 (bits 20) or ~6 (bits 19) candidates per 3 MiB tile, found by different waves and
+    # appended to the tile record in arrival order: compaction must sort them; every tile
+    # stays sparse (<= 15 stored candidates)
+    p = Ch.Params(average_bits=bits, seed=1, min=2000, max=30000)
     n = (9 << 20) + 77
     data = synthetic_bytes([0, n], 21)
     c = chunker_for(p)
