@@ -15,7 +15,10 @@ namespace pfscdc {
 #endif
 constexpr int kScanWaves = PFS_SCAN_WAVES;  // 12 = 3 per SIMD: LDS exactly full (8: 2 per SIMD, 3.5% slower)
 constexpr int kScanBlock = 64 * kScanWaves;
-constexpr int kStrip = 4096;
+#ifndef PFS_SCAN_STRIP
+#define PFS_SCAN_STRIP 4096
+#endif
+constexpr int kStrip = PFS_SCAN_STRIP;  // bytes per lane per tile (plus a 64-byte halo)
 constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
 constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
 constexpr uint32_t kTableLdsBytes = 256u * 256u;  // T x 32 bank-disjoint copies
