@@ -10,9 +10,11 @@
 //   1. cdc_scan_kernel     every byte: h_i = XOR_{k<64} rotl64(T[x_{i-k}], k), candidate iff
 //                          h_i & mask == 0.  Lane = 4 KiB strip, 64-byte halo re-read;
 //                          rolling recurrence; T replicated 32x in LDS so ds_read_b64 is
-//                          bank-conflict free; per 2 MiB tile <= 15 sorted candidates or a
-//                          DENSE flag.  HBM-bound by design (1 byte read per file byte).
-//   2. compact_kernel      one workgroup: prefix sum over tiles -> sorted candidate list.
+//                          bank-conflict free; per 3 MiB tile (12 waves) <= 15 candidates
+//                          appended to a global tile record, or a DENSE count.  Reads 1
+//                          byte per file byte; VALU-issue bound in practice.
+//   2. compact_kernel      one workgroup: prefix sum over tiles, each tile's offsets sorted
+//                          by rank -> sorted candidate list.
 //   3. select_kernel       one wave per file: serial cut selection over the sparse list
 //                          (writer.go:168,179 min/max rule), dense tiles re-rolled in-wave.
 //   4. segcompact_kernel   one workgroup: per-file segment counts -> dense segment list.
