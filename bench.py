@@ -72,9 +72,10 @@ def parse():
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
                     help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
-                         "one context + host thread each over the step's one input buffer)")
+                         "one context + host thread each over the step's one input buffer); "
+                         "0 = auto: 2 for --path put (fewer if HBM cannot hold 2 inputs), else 1")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -196,13 +197,29 @@ def main():
         sfiles = min(nfiles, max(1, int((4 << 30) // max(sizes[0], 1))))
     sbytes = int(offs[sfiles])
 
-    S = max(1, args.inflight)
-    chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
+    # Two steps in flight (two contexts on two streams, one resident input each): the next
+    # step's scan starts while this step's hash drains its longest chains (+6% at c2).
+    S = args.inflight if args.inflight > 0 else (2 if args.path == "put" else 1)
     batches = []
     for k in range(S if args.path != "commit" else 1):
-        t = torch.empty(total, dtype=torch.uint8, device=dev)
-        fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
+        try:
+            t = torch.empty(total, dtype=torch.uint8, device=dev)
+        except torch.OutOfMemoryError:
+            if k == 0 or args.inflight > 0:
+                raise
+            break
         batches.append(t)
+    if args.inflight == 0 and len(batches) > 1:
+        # keep headroom for the contexts' own device buffers (segments, entries, refs)
+        free, _ = torch.cuda.mem_get_info(dev)
+        if free < (4 << 30):
+            batches.pop()
+            torch.cuda.empty_cache()
+    if args.path != "commit":
+        S = len(batches)
+    chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
+    for k, t in enumerate(batches):
+        fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
     chunker, data = chunkers[0], batches[0]
     # all_gather_into_tensor needs equal blocks: the capacity of the largest shard
     cap = max(pd.max_segments(workload(args, world, r)[0], params.min_chunk) for r in range(world))
@@ -226,15 +243,19 @@ def main():
         last[k] = res
         return res
 
+    seq = [0]  # the context rotation continues across the warmup and timed runs: restarting
+    # it at context 0 after an odd warmup left the two steps serialised on the GPU
+
     def run(nsteps, record):
         for i in range(nsteps):
-            k = i % S
+            k = seq[0] % S
+            seq[0] += 1
             if pending[k]:
                 finish(k, record)
             chunkers[k].scan_async(batches[k], offs)
             pending[k] = True
-        for k in range(S):  # drain in launch order
-            kk = (nsteps + k) % S
+        for j in range(S):  # drain in launch order
+            kk = (seq[0] + j) % S
             if pending[kk]:
                 finish(kk, record)
 
@@ -330,6 +351,13 @@ def main():
 
     if gather and rank == 0 and "index" in last:
         out["dedup"] = hit_rate(last["index"])
+
+    # the timed steps are done: release the other steps' inputs and contexts (the e2e
+    # contexts below allocate their own device copies)
+    for k in range(1, len(chunkers)):
+        chunkers[k].close()
+    del batches[1:]
+    torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e:
         # one configs[1] batch (4 GiB) per call from pinned host memory
