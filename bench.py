@@ -219,7 +219,7 @@ def main():
         S = len(batches)
     chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
     for k, t in enumerate(batches):
-        fill(chunkers[k], t, sizes, fbase, seed + k, mode, np)
+        fill(chunkers[k], t, sizes, fbase, seed, mode, np)  # every step: the same workload
     chunker, data = chunkers[0], batches[0]
     # all_gather_into_tensor needs equal blocks: the capacity of the largest shard
     cap = max(pd.max_segments(workload(args, world, r)[0], params.min_chunk) for r in range(world))
