@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
                          "one context + host thread each over the step's one input buffer); "
-                         "0 = auto: 2 for --path put (fewer if HBM cannot hold 2 inputs), else 1")
+                         "0 = auto: 2 for --path put on c2/c3 (1 if HBM cannot hold 2 inputs), else 1")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -198,8 +198,11 @@ def main():
     sbytes = int(offs[sfiles])
 
     # Two steps in flight (two contexts on two streams, one resident input each): the next
-    # step's scan starts while this step's hash drains its longest chains (+6% at c2).
-    S = args.inflight if args.inflight > 0 else (2 if args.path == "put" else 1)
+    # step's scan starts while this step's hash drains its longest chains (c2 +6%, c3 2x).
+    # c4/c5 hashes are ~20K chains of up to 10.7 MB that already fill the GPU: two of them
+    # side by side only stretch each other (598-645 vs 667-669 GiB/s), so one step there.
+    S = args.inflight if args.inflight > 0 else (
+        2 if args.path == "put" and args.config in ("c2", "c3") else 1)
     batches = []
     for k in range(S if args.path != "commit" else 1):
         try:
