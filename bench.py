@@ -351,6 +351,20 @@ def main():
     }
     if rvalu:
         out["roofline_valu"] = rvalu
+    if S > 1:
+        # after the timed region: one step alone on the GPU, so the kernels' own durations
+        # (and rooflines) can be read beside the overlapped ones above
+        chunkers[0].scan_async(batches[0], offs)
+        chunkers[0].wait()
+        iso = {k: round(v, 4) for k, v in chunkers[0].timings().items()}
+        out["kernel_ms_isolated"] = iso
+        ri = roof(iso["hash"])
+        ri["kernel"] = "blake2b_kernel"
+        rc = roof(iso["scan"])
+        rc["kernel"] = "cdc_scan_kernel"
+        out["roofline_isolated"] = {"hash": ri, "scan": rc,
+                                    "note": "one step with nothing else in flight, after the "
+                                            "timed region; not the headline measurement"}
 
     if gather and rank == 0 and "index" in last:
         out["dedup"] = hit_rate(last["index"])
