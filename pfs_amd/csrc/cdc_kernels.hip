@@ -266,6 +266,10 @@ PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __r
   record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, rec);
 }
 
+#ifndef PFS_SCAN_DYN
+#define PFS_SCAN_DYN 1  // scan work units from a counter (1) or round-robin tiles (0)
+#endif
+
 #ifndef PFS_EXP_GAHEAD
 #define PFS_EXP_GAHEAD 10
 #endif
@@ -323,7 +327,7 @@ template <bool WIDE>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
-    TileRec* __restrict__ recs) {
+    TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr) {
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
   // images.  recs[] is zeroed before the launch; candidates are added to it directly.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -351,10 +355,25 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   }
   __syncthreads();  // table copies written; from here on every wave runs on its own
 
+#if PFS_SCAN_DYN
+  // Work unit = one wave's 64 strips of a tile.  Each wave takes the next unit from a
+  // launch-wide counter (zeroed before the launch), so CUs that start late (another step's
+  // hash still draining there) simply take fewer units instead of finishing last.
+  const uint64_t nunits = ntiles * (uint64_t)kScanWaves;
+  for (;;) {
+    uint32_t u0 = 0;
+    if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);
+    const uint64_t unit = (uint32_t)__builtin_amdgcn_readfirstlane(u0);
+    if (unit >= nunits) break;
+    const uint64_t tile = unit / kScanWaves;
+    const uint64_t wslot = unit % kScanWaves;
+#else
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t wslot = wave;
+#endif
     TileRec* const rec = recs + tile;
     const uint64_t tile_base = tile * kTile;
-    const uint64_t wave_base = tile_base + (uint64_t)wave * 64 * kStrip;
+    const uint64_t wave_base = tile_base + wslot * 64 * kStrip;
     if (wave_base < n) {  // wave-uniform
       const bool fast = wave_base + 64 * (uint64_t)kStrip <= n_main;
       auto dma_step = [&](uint32_t step) {
@@ -1437,7 +1456,7 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
 
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
-                       hipStream_t st) {
+                       uint32_t* unit_ctr, hipStream_t st) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   if (average_bits <= 32) {
@@ -1448,7 +1467,7 @@ hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, con
       attr = true;
     }
     cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
-                                                          mask64, ntiles, recs);
+                                                          mask64, ntiles, recs, unit_ctr);
   } else {
     static bool attr = false;
     if (!attr) {
@@ -1457,7 +1476,7 @@ hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, con
       attr = true;
     }
     cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
-                                                         mask64, ntiles, recs);
+                                                         mask64, ntiles, recs, unit_ctr);
   }
   return hipGetLastError();
 }

@@ -74,6 +74,7 @@ struct pfscdc_ctx {
   uint64_t* d_table = nullptr;
   DevBuf<uint8_t> d_data, d_tail;
   DevBuf<TileRec> d_recs;
+  DevBuf<uint32_t> d_unit_ctr;  // the scan's work-unit counter
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
@@ -217,6 +218,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_data.release();
   c->d_tail.release();
   c->d_recs.release();
+  c->d_unit_ctr.release();
   c->d_entries.release();
   c->d_counts.release();
   c->d_offs.release();
@@ -299,6 +301,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_qctr.ensure(2));
   if (options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
+  HIP_OK(c, c->d_unit_ctr.ensure(1));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
@@ -325,12 +328,13 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
   // the scan adds candidates to the tile records with atomics
   if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
+  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, sizeof(uint32_t), st));
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
   if (c->ntiles) {
     const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
-                          c->d_recs.p, grid, st));
+                          c->d_recs.p, grid, c->d_unit_ctr.p, st));
   }
   HIP_OK(c, hipEventRecord(c->ev[1], st));
   if (c->ntiles)

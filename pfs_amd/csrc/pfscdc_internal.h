@@ -81,7 +81,7 @@ uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
-                       hipStream_t st);
+                       uint32_t* unit_ctr, hipStream_t st);
 hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
                           uint64_t* n_entries, hipStream_t st);
 hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,
