@@ -84,6 +84,14 @@ const char* pfscdc_last_error(const pfscdc_ctx* ctx);
 /* Run every following GPU call of ctx on this hipStream_t (NULL = the ctx's own stream). */
 int pfscdc_set_stream(pfscdc_ctx* ctx, void* hip_stream);
 
+/* Ordering rule for device-resident inputs: the ctx's stream is a non-blocking stream of its
+ * own, so a device buffer written by work on another stream (a kernel, a non-blocking copy)
+ * must be ordered before a call that reads it.  pfscdc_stream_wait makes every following GPU
+ * call of ctx wait for the work already enqueued on hip_stream (NULL = the legacy default
+ * stream); it does not block the host.  The Python binding calls it with torch's current
+ * stream before each call on a torch tensor. */
+int pfscdc_stream_wait(pfscdc_ctx* ctx, void* hip_stream);
+
 /* CDC + content hash of a batch of files (one annotation each, concatenated).
  * Replaces, for every file of the batch, Writer.Annotate + Writer.Write + the hash part of
  * processChunk (writer.go:118-143,163-196,233-253,288-312): per-file cut positions and
@@ -340,6 +348,9 @@ uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w);
 /* Fileset i's Primitive (pointers valid until pfscdc_uw_destroy). */
 int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* out);
 int pfscdc_uw_destroy(pfscdc_uwriter* w);
+/* Message of the writer's sticky error (Put/Delete/Close or the background fileset write,
+ * with the data ctx's last error appended); "" while there is none. */
+const char* pfscdc_uw_last_error(const pfscdc_uwriter* w);
 
 /* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
 int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);

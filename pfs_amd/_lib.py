@@ -28,7 +28,8 @@ OPT_REF_IDS = 1
 # Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
 EXPORTED = [
     "pfscdc_default_params", "pfscdc_table", "pfscdc_go_int63", "pfscdc_ctx_create",
-    "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_scan",
+    "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_stream_wait",
+    "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
     "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms", "pfscdc_get_chunks",
@@ -38,7 +39,8 @@ EXPORTED = [
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
     "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
     "pfscdc_uw_create", "pfscdc_uw_put", "pfscdc_uw_delete", "pfscdc_uw_close",
-    "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_path_clean",
+    "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_uw_last_error",
+    "pfscdc_path_clean",
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
@@ -162,6 +164,7 @@ def load() -> C.CDLL:
             "pfscdc_ctx_destroy": (i32, [vp]),
             "pfscdc_last_error": (C.c_char_p, [vp]),
             "pfscdc_set_stream": (i32, [vp, vp]),
+            "pfscdc_stream_wait": (i32, [vp, vp]),
             "pfscdc_scan": (i32, [vp, vp, u64, i32, P(u64), u32]),
             "pfscdc_scan_async": (i32, [vp, vp, u64, i32, P(u64), u32]),
             "pfscdc_wait": (i32, [vp]),
@@ -197,6 +200,7 @@ def load() -> C.CDLL:
             "pfscdc_uw_num_filesets": (u32, [vp]),
             "pfscdc_uw_fileset": (i32, [vp, u32, P(FilesetInfo)]),
             "pfscdc_uw_destroy": (i32, [vp]),
+            "pfscdc_uw_last_error": (C.c_char_p, [vp]),
             "pfscdc_path_clean": (i32, [C.c_char_p, i32, C.c_char_p, u64]),
             "pfscdc_hash_data_refs": (i32, [vp, vp, u32, vp]),
             "pfscdc_store_create": (i32, [P(vp)]),

@@ -92,6 +92,18 @@ class Chunker:
     def set_stream(self, stream_handle: Optional[int]) -> None:
         self._check(self.lib.pfscdc_set_stream(self.ctx, stream_handle or None), "set_stream")
 
+    def _after_torch(self, *tensors) -> None:
+        """Order the ctx stream after torch's current stream (pfscdc_stream_wait) when a
+        call reads or writes torch CUDA tensors, so bytes written by a torch kernel or a
+        non-blocking copy have landed before the library's kernels read them."""
+        for t in tensors:
+            if t is not None and getattr(t, "is_cuda", False):
+                import torch
+
+                h = torch.cuda.current_stream(t.device).cuda_stream
+                self._check(self.lib.pfscdc_stream_wait(self.ctx, h or None), "stream_wait")
+                return
+
     def scan_async(self, data, file_offsets: Sequence[int]) -> None:
         """Enqueue a batch.  ``data``: bytes/bytearray/np.uint8 array (host) or a torch uint8
         CUDA tensor (device-resident, 16-byte aligned)."""
@@ -104,6 +116,7 @@ class Chunker:
                 raise ValueError("device data must be a contiguous uint8 tensor")
             ptr, nbytes, on_dev = data.data_ptr(), data.numel(), 1
             self._data_keep = data
+            self._after_torch(data)
         else:
             arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
                 else np.ascontiguousarray(data, dtype=np.uint8)
@@ -158,6 +171,7 @@ class Chunker:
         refs = np.ascontiguousarray(refs, dtype=_lib.ref_dtype())
         if len(refs) != n:
             raise ValueError("one ref per chunk")
+        self._after_torch(ctext, out)
         if hasattr(ctext, "is_cuda") and ctext.is_cuda:
             cptr, nbytes, con = ctext.data_ptr(), ctext.numel(), 1
         else:
@@ -221,6 +235,7 @@ class Chunker:
                                          if hash_known is not None else np.ones(n, np.uint8))
         if hasattr(data, "is_cuda") and data.is_cuda:
             ptr, nbytes, on = data.data_ptr(), data.numel(), 1
+            self._after_torch(data)
         else:
             arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
                                        if isinstance(data, (bytes, bytearray)) else data,
@@ -260,6 +275,7 @@ class Chunker:
                        mode: int = SYNTH_RANDOM) -> None:
         """Fill a torch uint8 CUDA tensor with the synthetic byte stream (see pfscdc.h)."""
         offs = _offsets_array(file_offsets)
+        self._after_torch(tensor)
         rc = self.lib.pfscdc_fill_synthetic_ex(self.ctx, tensor.data_ptr(),
                                                offs.ctypes.data_as(C.POINTER(C.c_uint64)),
                                                len(offs) - 1, seed, mode)

@@ -35,6 +35,16 @@
 
 #define PFS_DEV __device__ __forceinline__
 
+// Timing-only knobs (tools/ab_*.sh A/B builds) that drop the table lookup, the rotation, the
+// LDS address permute or the DMA wait: they produce wrong cuts and digests, so a build that
+// defines one must also say so explicitly; the product Makefile never does.
+#if defined(PFS_EXP_NO_TABLE) || defined(PFS_EXP_NO_ROT) || defined(PFS_EXP_NO_PERM) || \
+    defined(PFS_EXP_NO_DMA_WAIT)
+#ifndef PFS_TIMING_ONLY_BUILD
+#error "PFS_EXP_NO_* knobs give wrong results: define PFS_TIMING_ONLY_BUILD for a timing-only build"
+#endif
+#endif
+
 namespace pfscdc {
 
 // ------------------------------------------------------------------------------------------
@@ -1454,30 +1464,28 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
 // launchers (host)
 // ------------------------------------------------------------------------------------------
 
+// Per-device kernel attributes (the scan's 154 KB of dynamic LDS), set by pfscdc_ctx_create
+// on the ctx's device before any launch; idempotent, so every ctx sets them on its device.
+hipError_t prepare_kernels() {
+  const int lds = (int)kScanLdsBytes;
+  hipError_t e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)cdc_scan_kernel<true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, hipStream_t st) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
-  if (average_bits <= 32) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)cdc_scan_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr = true;
-    }
+  if (average_bits <= 32)
     cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
                                                           mask64, ntiles, recs, unit_ctr);
-  } else {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)cdc_scan_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr = true;
-    }
+  else
     cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
                                                          mask64, ntiles, recs, unit_ctr);
-  }
   return hipGetLastError();
 }
 

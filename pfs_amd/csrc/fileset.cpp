@@ -13,6 +13,7 @@
 //   chunk/chunk.proto, fileset/index/index.proto, chunk/util.go:25-30 (Reference)
 // Every chunk stream (the data writer of a serialized fileset and each index level) is a
 // pfscdc_writer: CDC, BLAKE2b and chunk.Create run on the GPU; this file is the bookkeeping.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -529,16 +530,23 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   std::mutex pool_mu;
   std::vector<Buffer> in_flight;             // the group the worker writes
   std::thread worker;
-  int worker_rc = PFSCDC_OK;
+  std::atomic<int> worker_rc{PFSCDC_OK};  // set by the background group write
   uint64_t pending_bytes = 0, inflight_bytes = 8ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
                         std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
   uint32_t next_fileset = 0;
   bool closed = false;
   int err = 0;
+  std::string errmsg;  // pfscdc_uw_last_error
 
-  int fail(int rc) {
-    if (!err) err = rc;
+  int fail(int rc, const char* what = nullptr) {
+    if (!err) {
+      err = rc;
+      errmsg = std::string(what ? what : "unordered writer") + " failed (status " +
+               std::to_string(rc) + ")";
+      const char* ce = pfscdc_last_error(st.data_ctx);
+      if (ce && *ce) errmsg += std::string(": ") + ce;
+    }
     return err;
   }
 
@@ -628,6 +636,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   }
 
   int put(const std::string& p, std::string tag, bool append, const uint8_t* data, uint64_t n) {
+    if (int rc = worker_rc.load()) return rc;  // the last group's write already failed
     if (tag.empty()) tag = "default";
     if (!append) buffer.del(p, tag);
     std::vector<Span>* w = &buffer.add(p, tag);
@@ -703,27 +712,34 @@ int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int appe
                   const void* data, uint64_t n) {
   if (!w || !path || (n && !data)) return PFSCDC_EINVAL;
   if (w->err) return w->err;
-  if (w->closed) return w->fail(PFSCDC_ESTATE);
+  if (w->closed) return w->fail(PFSCDC_ESTATE, "Put after Close");
   int rc = w->put(path, tag ? tag : "", append_file != 0, (const uint8_t*)data, n);
-  return rc ? w->fail(rc) : PFSCDC_OK;
+  return rc ? w->fail(rc, "Put") : PFSCDC_OK;
 }
 
 int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag) {
   if (!w || !path) return PFSCDC_EINVAL;
   if (w->err) return w->err;
-  if (w->closed) return w->fail(PFSCDC_ESTATE);
+  if (w->closed) return w->fail(PFSCDC_ESTATE, "Delete after Close");
   int rc = w->del(path, tag ? tag : "");
-  return rc ? w->fail(rc) : PFSCDC_OK;
+  return rc ? w->fail(rc, "Delete") : PFSCDC_OK;
 }
 
 int pfscdc_uw_close(pfscdc_uwriter* w) {
   if (!w) return PFSCDC_EINVAL;
+  // the background group write may still be appending to filesets: join it on every path
+  const int wrc = w->join();
   if (w->err) return w->err;
+  if (wrc) return w->fail(wrc, "Close (background fileset write)");
   if (w->closed) return PFSCDC_OK;
   w->closed = true;
   int rc = w->serialize();
   if (!rc) rc = w->flush_pending(false);
-  return rc ? w->fail(rc) : PFSCDC_OK;
+  return rc ? w->fail(rc, "Close") : PFSCDC_OK;
+}
+
+const char* pfscdc_uw_last_error(const pfscdc_uwriter* w) {
+  return w ? w->errmsg.c_str() : "null unordered writer";
 }
 
 uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w) {

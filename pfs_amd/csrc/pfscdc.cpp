@@ -86,6 +86,7 @@ struct pfscdc_ctx {
   float get_ms = 0.f;
   float create_ms = 0.f, create_hash_ms = 0.f;
   hipEvent_t cev = nullptr;  // create_refs: between the content-hash and the Ref.Id passes
+  hipEvent_t wev = nullptr;  // pfscdc_stream_wait: the caller's stream position
   std::vector<uint32_t> perm;  // create_refs: record -> chunk
   bool have_refs = false;
   bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
@@ -190,6 +191,11 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (hipError_t e = prepare_kernels(); e != hipSuccess) {
+    std::fprintf(stderr, "pfscdc_ctx_create: kernel attributes: %s\n", hipGetErrorString(e));
+    delete c;
+    return PFSCDC_EHIP;
+  }
   generate_hashes(params->seed, c->table);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&c->d_table, sizeof c->table) != hipSuccess ||
@@ -202,7 +208,8 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
       delete c;
       return PFSCDC_EHIP;
     }
-  if (hipEventCreate(&c->cev) != hipSuccess) {
+  if (hipEventCreate(&c->cev) != hipSuccess ||
+      hipEventCreateWithFlags(&c->wev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return PFSCDC_EHIP;
   }
@@ -240,6 +247,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->cev) (void)hipEventDestroy(c->cev);
+  if (c->wev) (void)hipEventDestroy(c->wev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PFSCDC_OK;
@@ -250,6 +258,16 @@ const char* pfscdc_last_error(const pfscdc_ctx* c) { return c ? c->err.c_str() :
 int pfscdc_set_stream(pfscdc_ctx* c, void* hip_stream) {
   if (!c) return PFSCDC_EINVAL;
   c->stream = hip_stream ? (hipStream_t)hip_stream : c->own_stream;
+  return PFSCDC_OK;
+}
+
+int pfscdc_stream_wait(pfscdc_ctx* c, void* hip_stream) {
+  if (!c) return PFSCDC_EINVAL;
+  hipStream_t s = (hipStream_t)hip_stream;
+  if (s == c->stream) return PFSCDC_OK;
+  HIP_OK(c, hipSetDevice(c->device));
+  HIP_OK(c, hipEventRecord(c->wev, s));
+  HIP_OK(c, hipStreamWaitEvent(c->stream, c->wev, 0));
   return PFSCDC_OK;
 }
 
@@ -270,6 +288,9 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
       return fail(c, PFSCDC_EINVAL, "file_offsets must be nondecreasing");
   if (bytes_on_device && ((uintptr_t)bytes & 15))
     return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  c->ntiles = (nbytes + kTile - 1) / kTile;
+  if (c->ntiles * (uint64_t)kScanWaves >= (1ull << 32))  // the scan's 32-bit work-unit counter
+    return fail(c, PFSCDC_EUNSUPPORTED, "batch too large for one scan (split it)");
   c->scan_valid = false;
   HIP_OK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
@@ -289,7 +310,6 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   c->slot_cap = cap;
   c->nfiles = nfiles;
   c->nbytes = nbytes;
-  c->ntiles = (nbytes + kTile - 1) / kTile;
 
   HIP_OK(c, c->d_offs.ensure(nfiles + 1));
   HIP_OK(c, c->d_seg_base.ensure(nfiles + 1));

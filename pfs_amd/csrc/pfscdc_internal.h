@@ -79,6 +79,7 @@ bool ctx_scan_valid(const pfscdc_ctx* ctx);
 uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
 uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
+hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, hipStream_t st);

@@ -99,7 +99,7 @@ class UnorderedWriter:
             exc, self._exc = self._exc, None
             raise exc
         if rc:
-            msg = self.lib.pfscdc_last_error(self._chunker.ctx)
+            msg = self.lib.pfscdc_uw_last_error(self._w) if getattr(self, "_w", None) else None
             raise _lib.PfsCdcError(rc, f"{what}: {msg.decode() if msg else ''}")
 
     def put(self, p: str, tag: str, append_file: bool, data) -> None:
