@@ -153,6 +153,30 @@ int pfscdc_last_create_ms(pfscdc_ctx* ctx, float* ms);
 /* Its split: out[0] content-hash pass, out[1] Ref.Id pass (order, dek, ChaCha20 + BLAKE2b). */
 int pfscdc_last_create_timings(pfscdc_ctx* ctx, float out[2]);
 
+/* ---- one stream split across GPUs (writer.go:163-189 block-parallel) --------
+ * A stream of N bytes is cut into equal byte ranges, one per GPU.  The rolling hash at a
+ * position is a pure function of the 64 bytes ending there, so each GPU finds the candidate
+ * positions of its range from its bytes plus the 64 bytes in front (the halo); the serial
+ * min/max selection then runs once over the gathered, sorted candidates (cheap: ~1 per 8 MiB),
+ * and each segment is hashed by the GPU whose range holds its first byte, after the bytes of a
+ * segment that straddles the border are copied over from the next range. */
+
+/* Candidates of one range: every position p of bytes (halo <= p < nbytes, p >= 63) where the
+ * buzhash64 of bytes [p-63, p] has (h & mask) == 0, sorted ascending, as offsets into bytes.
+ * halo (<= 64) = the bytes in front of the range copied from the previous one (0 at the
+ * stream start, where positions < 63 are never candidates: min >= 64 puts them before the
+ * first eligible cut).  out: cap entries; *n = the count (PFSCDC_ENOMEM if > cap, out holds
+ * the first cap).  Tiles with more than 15 candidates are re-rolled exactly on the host.
+ * Timings: pfscdc_last_timings out[0] (scan) and out[1] (compaction). */
+int pfscdc_candidates(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                      uint64_t halo, uint64_t* out, uint64_t cap, uint64_t* n);
+
+/* BLAKE2b-256 of n byte ranges [begins[i], begins[i] + sizes[i]) of bytes (device pointer,
+ * 16-B aligned, if bytes_on_device), into out (32 B each): the DataRef hashes of segments
+ * whose cuts were selected elsewhere (writer.go:240,301-312).  Synchronous. */
+int pfscdc_hash_ranges(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* begins, const uint64_t* sizes, uint32_t n, uint8_t* out);
+
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
  * positions inside dense tiles are reported through the tile marker instead.  Debug/test
  * hook for the candidate-scan kernel. */
@@ -183,6 +207,13 @@ int pfscdc_fill_synthetic(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* file
 #define PFSCDC_SYNTH_DEDUP_FILES 2u
 int pfscdc_fill_synthetic_ex(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* file_offsets,
                              uint32_t nfiles, uint64_t seed, uint32_t mode);
+/* The same bytes for pieces of files: piece i (bytes [piece_offsets[i], piece_offsets[i+1])
+ * of dev_bytes) holds bytes [file_starts[i], ...) of file file_ids[i] (NULL ids: file i;
+ * NULL starts: from byte 0).  A rank generates just its pieces of a commit whose files are
+ * cut across serialized filesets or ranks. */
+int pfscdc_fill_synthetic_pieces(pfscdc_ctx* ctx, void* dev_bytes, const uint64_t* piece_offsets,
+                                 uint32_t npieces, const uint32_t* file_ids,
+                                 const uint64_t* file_starts, uint64_t seed, uint32_t mode);
 
 /* ---- chunk.Writer mirror (writer.go:52-438) ------------------------------------------
  * A writer buffers annotated bytes in host memory, runs them through pfscdc_scan in

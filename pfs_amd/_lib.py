@@ -44,6 +44,7 @@ EXPORTED = [
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
+    "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
 ]
 
 
@@ -212,6 +213,10 @@ def load() -> C.CDLL:
             "pfscdc_writer_copy": (i32, [vp, P(FullDataRef)]),
             "pfscdc_writer_prefetch": (i32, [vp, P(FullDataRef), u32]),
             "pfscdc_merge_file_hash": (i32, [vp, vp, P(FullDataRef), u32, vp]),
+            "pfscdc_candidates": (i32, [vp, vp, u64, i32, u64, P(u64), u64, P(u64)]),
+            "pfscdc_hash_ranges": (i32, [vp, vp, u64, i32, P(u64), P(u64), u32, vp]),
+            "pfscdc_fill_synthetic_pieces": (i32, [vp, vp, P(u64), u32, P(C.c_uint32), P(u64),
+                                                   u64, u32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

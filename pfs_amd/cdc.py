@@ -266,10 +266,72 @@ class Chunker:
         self._check(self.lib.pfscdc_last_get_ms(self.ctx, C.byref(ms)), "get_ms")
         return ms.value
 
+    def candidates(self, data, halo: int = 0, cap: int = 1 << 16) -> np.ndarray:
+        """Sorted candidate positions of one range of a split stream (pfscdc_candidates):
+        offsets p >= halo into ``data`` (the range with ``halo`` bytes of the previous range
+        in front) where the rolling hash of bytes [p-63, p] passes the mask test."""
+        ptr, nbytes, on_dev = self._bytes_arg(data)
+        while True:
+            out = np.zeros(max(cap, 1), dtype=np.uint64)
+            n = C.c_uint64()
+            rc = self.lib.pfscdc_candidates(self.ctx, ptr, nbytes, on_dev, halo,
+                                            out.ctypes.data_as(C.POINTER(C.c_uint64)), cap,
+                                            C.byref(n))
+            if rc == _lib.PFSCDC_ENOMEM and n.value > cap:
+                cap = n.value
+                continue
+            self._check(rc, "candidates")
+            return out[:n.value].copy()
+
+    def hash_ranges(self, data, begins, sizes) -> np.ndarray:
+        """BLAKE2b-256 of byte ranges of ``data`` (pfscdc_hash_ranges): uint8[n, 32]."""
+        b = np.ascontiguousarray(np.asarray(begins, dtype=np.uint64))
+        z = np.ascontiguousarray(np.asarray(sizes, dtype=np.uint64))
+        if b.shape != z.shape:
+            raise ValueError("begins and sizes differ in length")
+        ptr, nbytes, on_dev = self._bytes_arg(data)
+        out = np.zeros((max(len(b), 1), 32), dtype=np.uint8)
+        rc = self.lib.pfscdc_hash_ranges(self.ctx, ptr, nbytes, on_dev,
+                                         b.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                         z.ctypes.data_as(C.POINTER(C.c_uint64)), len(b),
+                                         out.ctypes.data)
+        self._check(rc, "hash_ranges")
+        return out[:len(b)]
+
+    def _bytes_arg(self, data):
+        """(pointer, nbytes, on_device) of a torch CUDA tensor or host bytes; keeps the
+        host array alive on self for the call."""
+        if hasattr(data, "is_cuda") and data.is_cuda:
+            if data.dtype.itemsize != 1 or not data.is_contiguous():
+                raise ValueError("device data must be a contiguous uint8 tensor")
+            self._after_torch(data)
+            return data.data_ptr(), data.numel(), 1
+        arr = np.frombuffer(data, dtype=np.uint8) \
+            if isinstance(data, (bytes, bytearray, memoryview)) \
+            else np.ascontiguousarray(data, dtype=np.uint8)
+        self._arg_keep = arr
+        return (arr.ctypes.data if arr.size else None), arr.size, 0
+
     def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
         out = (C.c_uint64 * cap)()
         n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)
         return np.array(out[:min(n, cap)], dtype=np.uint64)
+
+    def fill_synthetic_pieces(self, tensor, piece_offsets: Sequence[int], file_ids, file_starts,
+                              seed: int, mode: int = SYNTH_RANDOM) -> None:
+        """Fill a torch uint8 CUDA tensor with pieces of synthetic files: piece i = bytes
+        [file_starts[i], ...) of file file_ids[i] (pfscdc_fill_synthetic_pieces)."""
+        offs = _offsets_array(piece_offsets)
+        ids = np.ascontiguousarray(np.asarray(file_ids, dtype=np.uint32))
+        st = np.ascontiguousarray(np.asarray(file_starts, dtype=np.uint64))
+        if len(ids) != len(offs) - 1 or len(st) != len(offs) - 1:
+            raise ValueError("one file id and start per piece")
+        self._after_torch(tensor)
+        rc = self.lib.pfscdc_fill_synthetic_pieces(
+            self.ctx, tensor.data_ptr(), offs.ctypes.data_as(C.POINTER(C.c_uint64)), len(ids),
+            ids.ctypes.data_as(C.POINTER(C.c_uint32)) if len(ids) else None,
+            st.ctypes.data_as(C.POINTER(C.c_uint64)) if len(st) else None, seed, mode)
+        self._check(rc, "fill_synthetic_pieces")
 
     def fill_synthetic(self, tensor, file_offsets: Sequence[int], seed: int,
                        mode: int = SYNTH_RANDOM) -> None:
@@ -303,6 +365,16 @@ def _synth_words(fid: int, w0: int, nw: int, seed: int) -> np.ndarray:
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return z.astype("<u8").view(np.uint8)
+
+
+def synthetic_piece_bytes(file_id: int, start: int, n: int, seed: int,
+                          mode: int = SYNTH_RANDOM) -> np.ndarray:
+    """Bytes [start, start + n) of synthetic file ``file_id`` (host mirror of
+    pfscdc_fill_synthetic_pieces for one piece)."""
+    if n == 0:
+        return np.zeros(0, dtype=np.uint8)
+    offs = np.array([0] * (file_id + 1) + [start + n], dtype=np.uint64)  # earlier files empty
+    return synthetic_bytes(offs, seed, mode)[start:start + n]
 
 
 def synthetic_bytes(file_offsets: Sequence[int], seed: int, mode: int = SYNTH_RANDOM) -> np.ndarray:

@@ -1429,8 +1429,12 @@ PFS_DEV uint64_t synth_byte_word(uint64_t f, uint64_t o, uint64_t seed, uint32_t
   return synth_word(f, o >> 3, seed);
 }
 
+// Local file f of the launch is bytes [starts[f], ...) of file ids[f] of the synthetic
+// commit (ids/starts NULL: file f from its first byte), so a rank can generate just its
+// pieces of files that are cut across serialized filesets or ranks.
 __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ offs,
-                             uint32_t nfiles, uint64_t seed, uint32_t mode) {
+                             uint32_t nfiles, const uint32_t* __restrict__ ids,
+                             const uint64_t* __restrict__ starts, uint64_t seed, uint32_t mode) {
   const uint64_t n = offs[nfiles];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 8;
   for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; g < n; g += stride) {
@@ -1447,8 +1451,9 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
       const uint64_t p = g + b;
       if (p >= n) break;
       while (f + 1 < nfiles && offs[f + 1] <= p) f++;
-      const uint64_t o = p - offs[f];
-      bytes[b] = (uint8_t)(synth_byte_word(f, o, seed, mode) >> (8 * (o & 7)));
+      const uint64_t o = p - offs[f] + (starts ? starts[f] : 0);
+      const uint64_t fid = ids ? ids[f] : f;
+      bytes[b] = (uint8_t)(synth_byte_word(fid, o, seed, mode) >> (8 * (o & 7)));
     }
     if (g + 8 <= n) {
       uint64_t w;
@@ -1599,9 +1604,9 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   return hipGetLastError();
 }
 
-hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
-                        uint32_t mode, hipStream_t st) {
-  synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, seed, mode);
+hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, const uint32_t* ids,
+                        const uint64_t* starts, uint64_t seed, uint32_t mode, hipStream_t st) {
+  synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, ids, starts, seed, mode);
   return hipGetLastError();
 }
 

@@ -81,6 +81,8 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
   DevBuf<pfscdc_ref> d_refs;
   DevBuf<uint8_t> d_out;  // get_chunks: plaintext when the caller's output is on the host
+  DevBuf<uint32_t> d_ids;  // fill_synthetic_pieces
+  DevBuf<uint64_t> d_starts;
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
   float get_ms = 0.f;
@@ -239,6 +241,8 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_refs.release();
   c->h_refs.release();
   c->d_out.release();
+  c->d_ids.release();
+  c->d_starts.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -624,6 +628,122 @@ int pfscdc_hash_data_refs(pfscdc_ctx* c, const uint8_t* hashes, uint32_t n, uint
   return PFSCDC_OK;
 }
 
+int pfscdc_candidates(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                      uint64_t halo, uint64_t* out, uint64_t cap, uint64_t* n) {
+  // The block-parallel half of Writer.roll (writer.go:163-189) for one range of a stream split
+  // across GPUs: the scan and compaction kernels, then the rare dense tiles (more than kTileK
+  // candidates in 3 MiB) re-rolled here on the host from the 64-byte windows, exactly.
+  if (!c || !n || (cap && !out) || (nbytes && !bytes)) return PFSCDC_EINVAL;
+  *n = 0;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "candidates during a pending scan");
+  if (bytes_on_device && ((uintptr_t)bytes & 15))
+    return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  if (halo > 64) return fail(c, PFSCDC_EINVAL, "halo must be at most 64 bytes");
+  const uint64_t ntiles = (nbytes + kTile - 1) / kTile;
+  if (ntiles * (uint64_t)kScanWaves >= (1ull << 32))
+    return fail(c, PFSCDC_EUNSUPPORTED, "range too large for one scan (split it)");
+  if (nbytes <= halo) return PFSCDC_OK;
+  c->scan_valid = false;
+  c->nsegs = 0;
+  c->have_refs = false;
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  HIP_OK(c, c->d_recs.ensure(ntiles));
+  HIP_OK(c, c->d_unit_ctr.ensure(1));
+  HIP_OK(c, c->d_entries.ensure(ntiles * kTileK + 1));
+  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->d_tail.ensure(kTailBytes));
+  const uint8_t* data;
+  if (bytes_on_device) {
+    data = (const uint8_t*)bytes;
+  } else {
+    HIP_OK(c, c->d_data.ensure(nbytes + 64));
+    HIP_OK(c, hipMemcpyAsync(c->d_data.p, bytes, nbytes, hipMemcpyHostToDevice, st));
+    data = c->d_data.p;
+  }
+  const uint64_t n_main = nbytes & ~63ULL;
+  HIP_OK(c, hipMemsetAsync(c->d_tail.p, 0, kTailBytes, st));
+  if (nbytes > n_main)
+    HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main, hipMemcpyDeviceToDevice, st));
+  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * ntiles, st));
+  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, sizeof(uint32_t), st));
+  HIP_OK(c, hipEventRecord(c->ev[0], st));
+  const int grid = (int)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus);
+  HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, c->params.average_bits, ntiles,
+                        c->d_recs.p, grid, c->d_unit_ctr.p, st));
+  HIP_OK(c, hipEventRecord(c->ev[1], st));
+  HIP_OK(c, launch_compact(c->d_recs.p, ntiles, nbytes, c->d_entries.p, c->d_counts.p, st));
+  HIP_OK(c, hipEventRecord(c->ev[2], st));
+  uint64_t ne = 0;
+  HIP_OK(c, hipMemcpyAsync(&ne, c->d_counts.p, sizeof ne, hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  std::vector<uint64_t> ent(ne);
+  if (ne)
+    HIP_OK(c, hipMemcpy(ent.data(), c->d_entries.p, ne * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  const uint64_t mask = c->params.average_bits >= 64 ? ~0ULL
+                                                     : ((1ULL << c->params.average_bits) - 1);
+  std::vector<uint8_t> win;
+  uint64_t k = 0;
+  auto emit = [&](uint64_t p) {
+    if (p < halo) return;  // the previous range's bytes
+    if (k < cap) out[k] = p;
+    k++;
+  };
+  for (uint64_t e : ent) {
+    if (!(e & kDenseBit)) {
+      emit(e);
+      continue;
+    }
+    // dense tile: every position of [ts, te] re-rolled from its 64-byte window
+    const uint64_t te = e & ~kDenseBit, ts = (te / kTile) * kTile;
+    const uint64_t a = ts >= 64 ? ts - 64 : 0;
+    win.resize(te + 1 - a);
+    HIP_OK(c, hipMemcpy(win.data(), data + a, win.size(), hipMemcpyDeviceToHost));
+    auto byte = [&](uint64_t p) -> uint64_t { return p >= a ? win[p - a] : 0; };
+    // h_{ts-1} = XOR_k rotl(T[x_{ts-1-k}], k): roll the 64 bytes before ts from a zero state
+    // (x_j = 0 before the range start, the reset window)
+    uint64_t h = 0;
+    for (int64_t i = 0; i < 64; i++) {
+      const int64_t p = (int64_t)ts - 64 + i;
+      h = ((h << 1) | (h >> 63)) ^ c->table[p >= 0 ? byte((uint64_t)p) : 0];
+    }
+    for (uint64_t p = ts; p <= te; p++) {
+      const uint64_t in = byte(p), outb = p >= 64 ? byte(p - 64) : 0;
+      h = ((h << 1) | (h >> 63)) ^ c->table[in] ^ c->table[outb];
+      if (p >= 63 && (h & mask) == 0) emit(p);
+    }
+  }
+  *n = k;
+  return k > cap ? fail(c, PFSCDC_ENOMEM, "candidate count exceeds cap") : PFSCDC_OK;
+}
+
+int pfscdc_hash_ranges(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* begins, const uint64_t* sizes, uint32_t n, uint8_t* out) {
+  if (!c || (n && (!begins || !sizes || !out)) || (nbytes && !bytes)) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "hash_ranges during a pending scan");
+  for (uint32_t i = 0; i < n; i++)
+    if (begins[i] > nbytes || sizes[i] > nbytes - begins[i])
+      return fail(c, PFSCDC_EINVAL, "range outside the buffer");
+  if (bytes_on_device && ((uintptr_t)bytes & 15))
+    return fail(c, PFSCDC_EINVAL, "device bytes must be 16-byte aligned");
+  if (n == 0) return PFSCDC_OK;
+  const uint8_t* data;
+  if (bytes_on_device) {
+    data = (const uint8_t*)bytes;
+  } else {
+    HIP_OK(c, hipSetDevice(c->device));
+    HIP_OK(c, c->d_data.ensure(nbytes + 64));
+    HIP_OK(c, hipMemcpyAsync(c->d_data.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
+    data = c->d_data.p;
+  }
+  HIP_OK(c, hipEventRecord(c->ev[3], c->stream));
+  int rc = hash_records_device(c, data, nbytes, begins, sizes, n, out);
+  if (rc) return rc;
+  HIP_OK(c, hipEventRecord(c->ev[4], c->stream));
+  return PFSCDC_OK;
+}
+
 int pfscdc_last_create_ms(pfscdc_ctx* c, float* ms) {
   if (!c || !ms) return PFSCDC_EINVAL;
   *ms = c->create_ms;
@@ -653,20 +773,44 @@ void pfscdc_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
-int pfscdc_fill_synthetic_ex(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
-                             uint32_t nfiles, uint64_t seed, uint32_t mode) {
-  if (!c || !file_offsets || (!dev_bytes && nfiles && file_offsets[nfiles])) return PFSCDC_EINVAL;
+int pfscdc_fill_synthetic_pieces(pfscdc_ctx* c, void* dev_bytes, const uint64_t* piece_offsets,
+                                 uint32_t npieces, const uint32_t* file_ids,
+                                 const uint64_t* file_starts, uint64_t seed, uint32_t mode) {
+  if (!c || !piece_offsets || (!dev_bytes && npieces && piece_offsets[npieces]))
+    return PFSCDC_EINVAL;
   if (mode > PFSCDC_SYNTH_DEDUP_FILES) return PFSCDC_EINVAL;
-  if (nfiles == 0 || file_offsets[nfiles] == 0) return PFSCDC_OK;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "fill during a pending scan");
+  if (npieces == 0 || piece_offsets[npieces] == 0) return PFSCDC_OK;
+  c->scan_valid = false;
   HIP_OK(c, hipSetDevice(c->device));
-  HIP_OK(c, c->h_offs.ensure(nfiles + 1));
-  HIP_OK(c, c->d_offs.ensure(nfiles + 1));
-  std::memcpy(c->h_offs.p, file_offsets, sizeof(uint64_t) * (nfiles + 1));
-  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (nfiles + 1),
+  HIP_OK(c, c->h_offs.ensure(npieces + 1));
+  HIP_OK(c, c->d_offs.ensure(npieces + 1));
+  std::memcpy(c->h_offs.p, piece_offsets, sizeof(uint64_t) * (npieces + 1));
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (npieces + 1),
                            hipMemcpyHostToDevice, c->stream));
-  HIP_OK(c, launch_synth((uint8_t*)dev_bytes, c->d_offs.p, nfiles, seed, mode, c->stream));
+  const uint32_t* ids = nullptr;
+  const uint64_t* starts = nullptr;
+  if (file_ids) {
+    HIP_OK(c, c->d_ids.ensure(npieces));
+    HIP_OK(c, hipMemcpy(c->d_ids.p, file_ids, sizeof(uint32_t) * npieces, hipMemcpyHostToDevice));
+    ids = c->d_ids.p;
+  }
+  if (file_starts) {
+    HIP_OK(c, c->d_starts.ensure(npieces));
+    HIP_OK(c, hipMemcpy(c->d_starts.p, file_starts, sizeof(uint64_t) * npieces,
+                        hipMemcpyHostToDevice));
+    starts = c->d_starts.p;
+  }
+  HIP_OK(c, launch_synth((uint8_t*)dev_bytes, c->d_offs.p, npieces, ids, starts, seed, mode,
+                         c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   return PFSCDC_OK;
+}
+
+int pfscdc_fill_synthetic_ex(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,
+                             uint32_t nfiles, uint64_t seed, uint32_t mode) {
+  return pfscdc_fill_synthetic_pieces(c, dev_bytes, file_offsets, nfiles, nullptr, nullptr, seed,
+                                      mode);
 }
 
 int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_offsets,

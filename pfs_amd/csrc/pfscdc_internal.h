@@ -105,7 +105,7 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
                       int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st);
-hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, uint64_t seed,
-                        uint32_t mode, hipStream_t st);
+hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, const uint32_t* ids,
+                        const uint64_t* starts, uint64_t seed, uint32_t mode, hipStream_t st);
 
 }  // namespace pfscdc
