@@ -3,31 +3,41 @@
 
 Metric: GiB/s of file bytes through CDC rolling hash + per-segment BLAKE2b-256 content hash
 with inputs already resident in HBM.  A "step" = one pass of the whole path over the step's
-files: candidate scan -> compaction -> cut selection -> LPT order -> BLAKE2b of every
-segment -> segment records back on the host (and, for N>1 or --config c5, the gather of the
-chunk-ref index: RCCL all-gather for N>1).
+files: candidate scan (+ compaction) -> cut selection (+ segment compaction, LPT order) ->
+BLAKE2b of every segment -> segment records back on the host (and, for N>1 or --config c5,
+the gather of the chunk-ref index: an RCCL all-gather for N>1).
 
 Workloads (--config, BASELINE.json configs[i]; all synthetic, generated in HBM):
   c2 (default, the headline): configs[1], batches of 1024 independent 4 MiB buffers.  One
      step = --group such batches (default 32 = 128 GiB resident), because BLAKE2b chains are
      serial and the hash needs ~16K+ segments in flight to fill the GPU.
-     N>1: every rank its own 32-batch shard (weak scaling).
-  c3: configs[2], one 10 GiB stream per GPU (block-parallel scan with halos; the serial cut
-     set is checked against the CPU oracle on the whole stream).
+     N>1: every rank its own 32-batch shard (weak scaling).  The literal one-batch rate is
+     reported beside it (``configs1_literal``).
+  c3: configs[2], one 10 GiB stream.  N=1: one scan of the stream.  N>1: the stream split in
+     equal byte ranges with a 64-byte halo, candidates all-gathered, the serial selection on
+     every rank, straddling segments' bytes sent point to point, segments hashed by the rank
+     holding their first byte (pfs_amd.distributed.stream_segments; strong scaling).
   c4: configs[3], a 100 GiB commit of 10,000 files (10,737,418 B each, +2,400 on the last),
-     sharded by file across ranks (strong scaling), RCCL all-gather of the chunk-ref index.
+     cut into serialized filesets of --mem-threshold bytes as pachd's UnorderedWriter does;
+     ranks take whole filesets (a file cut at a fileset border is two pieces), so the
+     gathered index equals N=1's.  --group G commits per step per rank (auto: enough for
+     >= 16K BLAKE2b chains per GPU).
   c5: configs[4], the c4 layout with dedup-heavy bytes: 1 MiB blocks, half of them copies of
      64 pooled blocks (--dedup blocks) or half of the files copies of 64 pooled files
      (--dedup files); reports the segment / byte dedup hit rate of the gathered index.
 
-Extra objects on the JSON line: ``roofline`` (dominant kernel, HIP events on the library's
-stream), ``roofline_cdc`` (the scan kernel), ``cpu_baseline`` (C restatement of the
-reference chunker on the host cores, rank 0 at N=1), ``e2e`` (pinned host input incl. PCIe
-H2D, c2 only), ``parity`` (GPU records == CPU oracle records on a sample of the workload).
+Extra objects on the JSON line: ``roofline`` (dominant kernel: its execution span measured
+inside the kernel, first wavefront start to last wavefront end, = a kernel trace's
+duration; traffic and VALU counts from the committed PMC pass of this command when one
+exists), ``roofline_cdc`` (the scan kernel), ``cpu_baseline`` (C restatement of the
+reference chunker on the host threads the box allots, rank 0 at N=1), ``e2e`` (pinned host
+input incl. PCIe H2D, c2 only), ``parity`` (GPU records == CPU oracle records on a sample).
 """
 import argparse
 import json
+import math
 import os
+import statistics
 import sys
 import time
 
@@ -35,12 +45,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# VALU issue ceiling: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 integer VOP3 instruction
-# (profiles/r1_ubench_issue_rates.txt: 4.1-4.3 cycles with 2-4 waves per SIMD)
+# VALU issue ceiling for the 4-cycle class of wave64 integer ops (VOP3 alignbit/perm/add3,
+# 64-bit adds, DPP forms, carry adds: 4.1-4.3 SIMD cycles each at 2 waves per SIMD;
+# profiles/r2/valu_issue.txt): 1024 SIMDs x 2.4 GHz / 4.  Plain 32-bit VOP2 ops (xor, add,
+# shifts) issue in ~2.1 cycles, so a kernel's own mix sets its exact ceiling.
 VALU_PEAK_GIPS = 1024 * 2.4 / 4.0
 GIB = float(1 << 30)
 C4_FILES, C4_FILE_BYTES, C4_TAIL = 10_000, 10_737_418, 2_400
 C3_BYTES = 10 * (1 << 30)
+MIN_CHAINS = 16384  # BLAKE2b chains per GPU per step for the hash to reach its issue bound
 
 
 def parse():
@@ -51,9 +64,10 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--files", type=int, default=1024, help="c2: files per configs[1] batch")
     ap.add_argument("--file-bytes", type=int, default=4 << 20, help="c2: bytes per file")
-    ap.add_argument("--group", type=int, default=32,
-                    help="c2: configs[1] batches per step (one launch group, resident in HBM "
-                         "together)")
+    ap.add_argument("--group", type=int, default=0,
+                    help="c2: configs[1] batches per step (default 32 = 128 GiB resident); "
+                         "c4/c5: commits per step per rank (default: enough for >= 16K "
+                         "chains per GPU); c3: 1")
     ap.add_argument("--dedup", default="blocks", choices=["blocks", "files"], help="c5 layout")
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
@@ -64,76 +78,132 @@ def parse():
                          "decrypt), §8 next row 3, device-resident in and out; commit: the "
                          "pachd data plane, §8 next rows 1-3: files cut into filesets at "
                          "--mem-threshold bytes, one chunk.Writer stream per fileset (Annotate "
-                         "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk")
+                         "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk; "
+                         "uw: host-fed UnorderedWriter with indexes; rechunk: Writer.Copy")
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
     ap.add_argument("--rechunk-writers", type=int, default=10,
                     help="rechunk: writers the file was written by (TestStableHash shape)")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
-                    help="commit: UnorderedWriter memThreshold (storage.go:23, 1e9)")
+                    help="UnorderedWriter memThreshold (fileset/storage.go:23, 1e9): the "
+                         "serialized-fileset size of c4/c5 and of --path commit/uw")
     ap.add_argument("--seed", type=int, default=-1, help="data seed (default: per config)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
                          "one context + host thread each over the step's one input buffer); "
                          "0 = auto: 2 for --path put on c2/c3 (1 if HBM cannot hold 2 inputs), else 1")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the host threads the box allots (OMP_NUM_THREADS), else the "
+                         "affinity mask")
+    ap.add_argument("--cpu-batches", type=int, default=8,
+                    help="c2: configs[1] batches in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default="", help="per-launch HBM bytes from a PMC run")
+    ap.add_argument("--no-literal", action="store_true",
+                    help="c2: skip the one-batch (unaggregated configs[1]) measurement")
+    ap.add_argument("--traffic-json", default="",
+                    help="per-launch HBM bytes / VALU counts from a PMC run (default: the "
+                         "committed profiles/r2 pass of this workload, if any)")
     return ap.parse_args()
 
 
+class Work:
+    """This rank's input for one step: pieces (files or pieces of files) with their synthetic
+    file ids and starts, the global id of its first piece, and the layout info."""
+
+    def __init__(self, sizes, ids, starts, seed, mode, info, scaling, gbase=0, group=1,
+                 per_copy=None):
+        import numpy as np
+        self.sizes = [int(x) for x in sizes]
+        self.ids = np.asarray(ids, dtype=np.uint32)
+        self.starts = np.asarray(starts, dtype=np.uint64)
+        self.seed, self.mode, self.info, self.scaling = seed, mode, info, scaling
+        self.gbase, self.group = gbase, group
+        self.per_copy = per_copy if per_copy is not None else len(self.sizes)
+        self.offs = np.zeros(len(self.sizes) + 1, dtype=np.uint64)
+        self.offs[1:] = np.cumsum(np.asarray(self.sizes, dtype=np.uint64))
+        # global id of every local piece in the gathered index (copy g of a commit: ids
+        # g * pieces_per_commit + piece)
+        self.gid = np.arange(len(self.sizes), dtype=np.uint64) + np.uint64(gbase)
+
+    @property
+    def total(self) -> int:
+        return int(self.offs[-1])
+
+
+def auto_group(chains_per_copy: int, bytes_per_copy: int, cap: int = 8,
+               hbm_budget: int = 180 << 30) -> int:
+    """Copies per step so the GPU holds >= MIN_CHAINS BLAKE2b chains, within HBM."""
+    g = max(1, math.ceil(MIN_CHAINS / max(chains_per_copy, 1)))
+    return max(1, min(g, cap, hbm_budget // max(bytes_per_copy, 1)))
+
+
 def workload(args, world, rank):
-    """This rank's files for one step: (sizes, global id of its first file, seed, synth
-    mode, config info, scaling)."""
+    """This rank's pieces for one step."""
+    import numpy as np
+
     from pfs_amd import distributed as pd
     from pfs_amd.cdc import SYNTH_DEDUP_BLOCKS, SYNTH_DEDUP_FILES, SYNTH_RANDOM
 
     if args.config == "c2":
-        G = max(1, args.group)
+        G = args.group if args.group > 0 else 32
         n = args.files * G
-        seed = 0xC2 if args.seed < 0 else args.seed
+        seed = (0xC2 if args.seed < 0 else args.seed) + 1000 * rank
         info = {"workload": "configs[1]: batches of %d x %d B independent buffers; %d batches "
                             "per step (one launch group) per GPU" % (args.files, args.file_bytes, G),
                 "files_per_step": n, "file_bytes": args.file_bytes, "batches_per_step": G}
-        return [args.file_bytes] * n, 0, seed + 1000 * rank, SYNTH_RANDOM, info, "weak"
+        return Work([args.file_bytes] * n, np.arange(n), np.zeros(n), seed, SYNTH_RANDOM, info,
+                    "weak", gbase=rank * n, group=G, per_copy=args.files)
     if args.config == "c3":
         seed = 0xC3 if args.seed < 0 else args.seed
-        info = {"workload": "configs[2]: one %d B stream per GPU" % C3_BYTES,
-                "files_per_step": 1, "file_bytes": C3_BYTES}
-        return [C3_BYTES], 0, seed + 1000 * rank, SYNTH_RANDOM, info, "weak"
+        a, b = pd.split_stream(C3_BYTES, world)[rank]
+        info = {"workload": "configs[2]: one %d B stream%s" % (
+                    C3_BYTES, "" if world == 1 else ", split in %d equal byte ranges with a "
+                    "64-byte halo (candidates gathered, serial select, border segments sent "
+                    "point to point)" % world),
+                "files_per_step": 1, "file_bytes": C3_BYTES, "range": [a, b]}
+        return Work([b - a], [0], [a], seed, SYNTH_RANDOM, info,
+                    "weak" if world == 1 else "strong")
+    # c4 / c5: the commit as pachd serializes it, whole filesets per rank
     sizes = [C4_FILE_BYTES] * C4_FILES
     sizes[-1] += C4_TAIL
-    b, e = pd.shard_files(sizes, world)[rank]
+    lay = pd.commit_layout(sizes, args.mem_threshold)
+    fs = pd.shard_filesets(lay, world)[rank]
+    p0, p1 = pd.rank_pieces(lay, fs)
     mode = SYNTH_RANDOM
     if args.config == "c5":
         mode = SYNTH_DEDUP_BLOCKS if args.dedup == "blocks" else SYNTH_DEDUP_FILES
     seed = (0xC4 if args.config == "c4" else 0xC5) if args.seed < 0 else args.seed
+    psz = lay.size[p0:p1]
+    nbytes = int(psz.sum())
+    chains = int(np.sum(np.where(psz > 0, psz // 8_400_000 + 1, 0)))  # ~8.4 MB mean segment
+    G = args.group if args.group > 0 else auto_group(chains, nbytes)
     what = "100 GiB" if args.config == "c4" else "100 GiB dedup-heavy (%s)" % args.dedup
-    info = {"workload": "configs[%d]: %s commit of %d files (%d B each, +%d on the last), "
-                        "sharded by file over %d GPU(s)"
+    info = {"workload": "configs[%d]: %s commit of %d files (%d B each, +%d on the last), cut "
+                        "into serialized filesets of %d B (UnorderedWriter), whole filesets "
+                        "per GPU over %d GPU(s); %d commit(s) per step per GPU"
                         % (3 if args.config == "c4" else 4, what, C4_FILES, C4_FILE_BYTES,
-                           C4_TAIL, world),
-            "files_per_step": e - b, "files_total": C4_FILES}
+                           C4_TAIL, args.mem_threshold, world, G),
+            "filesets": lay.nfilesets, "filesets_this_rank": fs[1] - fs[0],
+            "pieces_per_commit": lay.npieces, "files_per_step": (p1 - p0) * G,
+            "commits_per_step": G, "files_total": C4_FILES}
     if args.config == "c5":
         info["dedup"] = ("1 MiB blocks, p=1/2 a copy of one of 64 pooled blocks"
                          if args.dedup == "blocks" else
                          "whole files, p=1/2 a copy of one of 64 pooled files")
-    return sizes[b:e], b, seed, mode, info, "strong"
+    # copy g of the commit: the same layout over files g * 10000 + f (its own bytes)
+    ids = np.concatenate([lay.file[p0:p1].astype(np.int64) + g * C4_FILES for g in range(G)])
+    starts = np.tile(lay.start[p0:p1], G)
+    w = Work(np.tile(psz, G), ids, starts, seed, mode, info, "strong" if G == 1 else "weak",
+             gbase=p0, group=G, per_copy=p1 - p0)
+    w.gid = np.concatenate([np.arange(p0, p1, dtype=np.uint64) + np.uint64(g * lay.npieces)
+                            for g in range(G)]) if p1 > p0 else w.gid
+    w.layout, w.fs_range = lay, fs
+    return w
 
 
-def fill(chunker, tensor, sizes, fbase, seed, mode, np):
-    """Generate this rank's files; file f of the shard is file fbase + f of the commit (the
-    generator keys bytes by file index, so empty files are put in front of the shard)."""
-    offs = np.zeros(fbase + len(sizes) + 1, dtype=np.uint64)
-    offs[fbase + 1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
-    chunker.fill_synthetic(tensor, offs, seed, mode)
-
-
-def local_index(segments, fbase):
-    out = segments.copy()
-    out["file"] = out["file"] + fbase
-    return out
+def fill(chunker, tensor, work):
+    chunker.fill_synthetic_pieces(tensor, work.offs, work.ids, work.starts, work.seed, work.mode)
 
 
 def hit_rate(index):
@@ -151,6 +221,46 @@ def hit_rate(index):
     nb = int(index["size"].sum()) if len(index) else 0
     return {"segments": int(len(index)), "segment_hit_rate": round(hit_s / max(len(index), 1), 5),
             "byte_hit_rate": round(hit_b / max(nb, 1), 5), "unique_digests": len(seen)}
+
+
+def host_threads() -> int:
+    """Host threads for the CPU baseline: the box's share (OMP_NUM_THREADS, 16 per GPU on the
+    GPU pool), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    return min(omp, aff) if omp > 0 else aff
+
+
+def cpu_model() -> str:
+    import platform
+    m = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return m
+
+
+def load_traffic(args, work):
+    """Per-launch PMC figures (FETCH_SIZE bytes, SQ_INSTS_VALU) of this exact workload."""
+    path = args.traffic_json
+    if not path and args.config == "c2" and work.group == 32 and args.files == 1024 \
+            and args.file_bytes == 4 << 20 and args.path == "put" and not args.ref_ids:
+        path = os.path.join(ROOT, "profiles", "r2", "traffic_c2.json")
+    if path and os.path.exists(path):
+        tj = json.load(open(path))
+        tj["_source"] = os.path.relpath(path, ROOT)
+        return tj
+    return None
+
+
+def med(xs):
+    return round(statistics.median(xs), 4) if xs else None
 
 
 def main():
@@ -179,32 +289,31 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
-    cdev = torch.device("cpu") if rehearse else dev  # collectives' tensors
+    cdev = None if rehearse else dev  # collectives' tensors: device (RCCL) or host (gloo)
+    ctx = {"np": np, "torch": torch, "dist": dist, "dev": dev, "cdev": cdev, "world": world,
+           "rank": rank, "local": local, "pd": pd}
 
     params = ChunkParams()  # reference defaults: avgBits 23, seed 1, min 1 MB, max 20 MB
-    sizes, fbase, seed, mode, info, scaling = workload(args, world, rank)
-    nfiles = len(sizes)
-    offs = np.zeros(nfiles + 1, dtype=np.uint64)
-    offs[1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
-    total = int(offs[-1])
-    # parity / CPU-baseline sample: the first configs[1] batch (c2), the whole stream (c3),
-    # or the shard's first ~4 GiB of files (c4/c5)
-    if args.config == "c2":
-        sfiles = min(args.files, nfiles)
-    elif args.config == "c3":
-        sfiles = 1
-    else:
-        sfiles = min(nfiles, max(1, int((4 << 30) // max(sizes[0], 1))))
-    sbytes = int(offs[sfiles])
+    ctx["params"] = params
+    if args.path == "uw":
+        return bench_uw(args, ctx)
+    if args.path == "rechunk":
+        return bench_rechunk(args, ctx)
+    if args.path == "commit":
+        return bench_commit(args, ctx)
+    if args.config == "c3" and world > 1 and args.path == "put":
+        return bench_c3_split(args, ctx)
+
+    work = workload(args, world, rank)
+    total = work.total
 
     # Two steps in flight (two contexts on two streams, one resident input each): the next
     # step's scan starts while this step's hash drains its longest chains (c2 +6%, c3 2x).
-    # c4/c5 hashes are ~20K chains of up to 10.7 MB that already fill the GPU: two of them
-    # side by side only stretch each other (598-645 vs 667-669 GiB/s), so one step there.
+    # c4/c5 hold >= 16K chains per step through --group instead.
     S = args.inflight if args.inflight > 0 else (
         2 if args.path == "put" and args.config in ("c2", "c3") else 1)
     batches = []
-    for k in range(S if args.path != "commit" else 1):
+    for k in range(S):
         try:
             t = torch.empty(total, dtype=torch.uint8, device=dev)
         except torch.OutOfMemoryError:
@@ -218,19 +327,21 @@ def main():
         if free < (4 << 30):
             batches.pop()
             torch.cuda.empty_cache()
-    if args.path != "commit":
-        S = len(batches)
+    S = len(batches)
     chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
     for k, t in enumerate(batches):
-        fill(chunkers[k], t, sizes, fbase, seed, mode, np)  # every step: the same workload
+        fill(chunkers[k], t, work)  # every step: the same workload
+    if args.path == "get":
+        return bench_get(args, ctx, chunkers[0], batches[0], work)
+
     chunker, data = chunkers[0], batches[0]
     # all_gather_into_tensor needs equal blocks: the capacity of the largest shard
-    cap = max(pd.max_segments(workload(args, world, r)[0], params.min_chunk) for r in range(world))
-    gather = world > 1 or args.config == "c5"
+    cap = max(pd.max_segments(workload(args, world, r).sizes, params.min_chunk)
+              for r in range(world)) if world > 1 else 0
+    gather = world > 1 or args.config != "c2"  # the commit's / stream's index on rank 0
     torch.cuda.synchronize()
-    acc = {"scan": 0.0, "compact": 0.0, "select": 0.0, "hash": 0.0, "total": 0.0}
-    if args.ref_ids:
-        acc["ref_ids"] = 0.0
+    steps_t = []   # per timed step: the library's timings dict
+    done_at = []   # completion times of the timed steps
     pending = [False] * S
     last = {}
 
@@ -238,11 +349,12 @@ def main():
         res = chunkers[k].wait()
         pending[k] = False
         if gather:
-            last["index"] = pd.gather_index(res.segments, fbase, cap, device=cdev) \
-                if world > 1 else local_index(res.segments, fbase)
+            segs = res.segments.copy()
+            segs["file"] = work.gid[segs["file"]].astype(np.uint32)
+            last["index"] = pd.gather_index(segs, 0, cap, device=cdev) if world > 1 else segs
         if record:
-            for name, v in chunkers[k].timings().items():
-                acc[name] += v
+            steps_t.append(chunkers[k].timings())
+            done_at.append(time.perf_counter())
         last[k] = res
         return res
 
@@ -250,30 +362,17 @@ def main():
     # it at context 0 after an odd warmup left the two steps serialised on the GPU
 
     def run(nsteps, record):
-        for i in range(nsteps):
+        for _ in range(nsteps):
             k = seq[0] % S
             seq[0] += 1
             if pending[k]:
                 finish(k, record)
-            chunkers[k].scan_async(batches[k], offs)
+            chunkers[k].scan_async(batches[k], work.offs)
             pending[k] = True
         for j in range(S):  # drain in launch order
             kk = (seq[0] + j) % S
             if pending[kk]:
                 finish(kk, record)
-
-    if args.path == "get":
-        return bench_get(args, world, rank, local, dev, chunkers[0], batches[0], offs, total,
-                         info, scaling, params, np, torch, dist)
-    if args.path == "rechunk":
-        return bench_rechunk(args, world, rank, dev, chunkers[0], batches[0], info, scaling,
-                             params, np, torch, dist)
-    if args.path == "uw":
-        return bench_uw(args, world, rank, dev, chunkers[0], batches[0], sizes, info, scaling,
-                        params, np, torch, dist)
-    if args.path == "commit":
-        return bench_commit(args, world, rank, dev, chunkers, batches[0], sizes, total, info,
-                            scaling, params, np, torch, dist)
 
     run(args.warmup, False)
     if world > 1:
@@ -296,78 +395,107 @@ def main():
         bytes_step = int(bt.item())
 
     K = max(args.steps, 1)
-    avg = {k: v / K for k, v in acc.items()}
     value = float(bytes_step) * args.steps / elapsed / GIB
     ms_per_step = elapsed * 1e3 / K
+    intervals = [(b - a) * 1e3 for a, b in zip([t0] + done_at[:-1], done_at)]
+    kmed = {name: med([s[name] for s in steps_t]) for name in steps_t[0]} if steps_t else {}
+    kmean = {name: round(sum(s[name] for s in steps_t) / len(steps_t), 4)
+             for name in steps_t[0]} if steps_t else {}
+    tj = load_traffic(args, work)
 
-    def roof(ms):
-        ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-                "bytes_per_launch": total, "avg_launch_ms": round(ms, 4)}
+    def roof(ms, kernel, traffic_key=None):
+        ach = total / (ms * 1e-3) / 1e9 if ms and ms > 0 else 0.0
+        r = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+             "bytes_per_launch": total, "avg_launch_ms": round(ms, 4) if ms else None,
+             "kernel": kernel}
+        if tj and traffic_key and tj.get(traffic_key):
+            r["traffic"] = tj[traffic_key]
+            r["traffic_source"] = tj["_source"] + " (FETCH_SIZE x 2, per launch)"
+        return r
 
-    dom = "hash" if avg["hash"] >= avg["scan"] else "scan"
-    roofline = roof(avg[dom])
-    roofline["kernel"] = {"hash": "blake2b_kernel", "scan": "cdc_scan_kernel"}[dom]
-    if args.ref_ids and avg["ref_ids"] > avg[dom]:
-        roofline = roof(avg["ref_ids"])
-        roofline["kernel"] = "blake2b_kernel<true> (ChaCha20 + BLAKE2b of the ciphertext)"
-    roofline_cdc = roof(avg["scan"])
-    roofline_cdc["kernel"] = "cdc_scan_kernel"
+    # the dominant kernel's duration = its execution span inside the kernel (first wavefront
+    # start to last wavefront end), averaged over the timed launches, as a kernel trace reports
+    hash_ms = kmean.get("hash_span") or kmean.get("hash")
+    scan_ms = kmean.get("scan_span") or kmean.get("scan")
+    dom_hash = (hash_ms or 0) >= (scan_ms or 0)
+    roofline = roof(hash_ms, "blake2b_kernel", "blake2b_kernel") if dom_hash else \
+        roof(scan_ms, "cdc_scan_kernel", "cdc_scan_kernel")
+    roofline["duration_source"] = ("in-kernel s_memrealtime span (first wave start to last wave "
+                                   "end), mean over the %d timed launches" % len(steps_t))
+    roofline["event_ms"] = kmean.get("hash" if dom_hash else "scan")
+    if args.ref_ids and kmean.get("ref_ids", 0) > (hash_ms or 0):
+        roofline = roof(kmean["ref_ids"], "blake2b_kernel<kModeRefId> (ChaCha20 + BLAKE2b of "
+                                          "the ciphertext; HIP events)")
+    roofline_cdc = roof(scan_ms, "cdc_scan_kernel (its last workgroup compacts the candidates)",
+                        "cdc_scan_kernel")
     rvalu = {}
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        tj = json.load(open(args.traffic_json))
-        roofline["traffic"] = tj.get(roofline["kernel"])
-        roofline_cdc["traffic"] = tj.get("cdc_scan_kernel")
-        # the ceiling that binds both kernels: VALU issue (instructions from the PMC pass)
-        for kern, ms in (("blake2b_kernel", avg["hash"]), ("cdc_scan_kernel", avg["scan"])):
+    if tj:
+        for kern, ms in (("blake2b_kernel", hash_ms), ("cdc_scan_kernel", scan_ms)):
             n = tj.get(kern + "_valu")
-            if n and ms > 0:
+            if n and ms:
                 ach = n / (ms * 1e-3) / 1e9
                 rvalu[kern] = {"bound": "valu-issue", "achieved": round(ach, 1),
                                "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
-                               "frac": round(ach / VALU_PEAK_GIPS, 4), "valu_per_launch": n}
+                               "frac": round(ach / VALU_PEAK_GIPS, 4), "valu_per_launch": n,
+                               "source": tj["_source"]}
 
+    info = dict(work.info)
     info.update({"steps_in_flight": S,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},
-                 "parallelism": "file-sharded x%d, RCCL all-gather of chunk-ref index" % world
+                 "parallelism": ("file-sharded x%d, RCCL all-gather of chunk-ref index" % world
+                                 if args.config == "c2" else
+                                 "fileset-sharded x%d, RCCL all-gather of chunk-ref index" % world)
                  if world > 1 else "single GPU"})
     out = {
         "metric": "GiB/s device-resident CDC rolling-hash + chunk content-hash",
         "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "scaling": work.scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)",
         "ref_ids": bool(args.ref_ids),
         "config": info,
         "segments_per_step": int(len(res.segments)),
-        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
-        "note": "kernel_ms / roofline durations are per step on this rank (HIP events on the "
-                "library's stream); the hash is VALU-issue bound, not HBM bound (DESIGN.md §4)",
-        "cdc_only_gib_s": round(total / (avg["scan"] * 1e-3) / GIB, 2) if avg["scan"] else None,
+        "ms_per_step_median": med(intervals),
+        "kernel_ms": kmean,
+        "kernel_ms_median": kmed,
+        "note": "kernel_ms: per step on this rank; scan/select/hash = HIP events on the "
+                "library's stream (they include waiting for CUs behind the other step in "
+                "flight), scan_span/hash_span = the kernels' own execution spans; the hash "
+                "is VALU-issue bound, not HBM bound (DESIGN.md §4)",
+        "cdc_only_gib_s": round(total / (scan_ms * 1e-3) / GIB, 2) if scan_ms else None,
         "roofline": roofline,
         "roofline_cdc": roofline_cdc,
     }
     if rvalu:
         out["roofline_valu"] = rvalu
     if S > 1:
-        # after the timed region: one step alone on the GPU, so the kernels' own durations
-        # (and rooflines) can be read beside the overlapped ones above
-        chunkers[0].scan_async(batches[0], offs)
-        chunkers[0].wait()
-        iso = {k: round(v, 4) for k, v in chunkers[0].timings().items()}
-        out["kernel_ms_isolated"] = iso
-        ri = roof(iso["hash"])
-        ri["kernel"] = "blake2b_kernel"
-        rc = roof(iso["scan"])
-        rc["kernel"] = "cdc_scan_kernel"
+        # after the timed region: steps alone on the GPU (median of 3), so the kernels' own
+        # durations can be read beside the overlapped ones above
+        iso = []
+        for _ in range(3):
+            chunkers[0].scan_async(batches[0], work.offs)
+            chunkers[0].wait()
+            iso.append(chunkers[0].timings())
+        im = {name: med([s[name] for s in iso]) for name in iso[0]}
+        out["kernel_ms_isolated"] = im
+        ri = roof(im["hash_span"], "blake2b_kernel")
+        rc = roof(im["scan_span"], "cdc_scan_kernel")
         out["roofline_isolated"] = {"hash": ri, "scan": rc,
-                                    "note": "one step with nothing else in flight, after the "
-                                            "timed region; not the headline measurement"}
+                                    "note": "median of 3 steps with nothing else in flight, "
+                                            "after the timed region"}
 
     if gather and rank == 0 and "index" in last:
-        out["dedup"] = hit_rate(last["index"])
+        idx = last["index"]
+        if args.config in ("c4", "c5"):  # the commit itself: copy 0 of every rank
+            idx = idx[idx["file"] < work.layout.npieces]
+        if args.config == "c5":
+            out["dedup"] = hit_rate(idx)
+        # the gathered chunk-ref index of the commit / stream: equal at every N
+        out["index_digest"] = __import__("hashlib").blake2b(idx.tobytes(),
+                                                            digest_size=16).hexdigest()
+        out["index_segments"] = int(len(idx))
 
     # the timed steps are done: release the other steps' inputs and contexts (the e2e
     # contexts below allocate their own device copies)
@@ -376,107 +504,13 @@ def main():
     del batches[1:]
     torch.cuda.empty_cache()
 
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_literal:
+        out["configs1_literal"] = literal_batch(args, work, chunker, data, params, local,
+                                                Chunker, torch)
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e:
-        # one configs[1] batch (4 GiB) per call from pinned host memory
-        host = torch.empty(sbytes, dtype=torch.uint8, pin_memory=True)
-        host.copy_(data[:sbytes])
-        hnp = host.numpy()
-        boffs = offs[:sfiles + 1]
-        e2e_chunker = Chunker(params, device=local)
-        e2e_chunker.scan(hnp, boffs)
-        torch.cuda.synchronize()
-        n_e2e = 2
-        t0 = time.perf_counter()
-        for _ in range(n_e2e):
-            e2e_chunker.scan(hnp, boffs)
-        te = (time.perf_counter() - t0) / n_e2e
-        # pipelined: two contexts (two streams) alternate, so batch k+1's H2D copy runs
-        # while batch k hashes
-        pipe = [e2e_chunker, Chunker(params, device=local)]
-        pipe[1].scan(hnp, boffs)
-        n_pipe, busy = 8, [False, False]
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(n_pipe):
-            k = i % 2
-            if busy[k]:
-                pipe[k].wait()
-            pipe[k].scan_async(hnp, boffs)
-            busy[k] = True
-        for k in range(2):
-            if busy[(n_pipe + k) % 2]:
-                pipe[(n_pipe + k) % 2].wait()
-        tp = (time.perf_counter() - t0) / n_pipe
-        out["e2e"] = {"value": round(sbytes / tp / GIB, 3), "unit": "GiB/s",
-                      "ms_per_batch": round(tp * 1e3, 3),
-                      "serial_value": round(sbytes / te / GIB, 3),
-                      "note": "configs[1] batches from pinned host memory (hipMemcpyAsync H2D + "
-                              "kernels + records D2H), two contexts on two streams alternating "
-                              "so each batch's copy overlaps the previous batch's kernels; "
-                              "serial_value: one batch at a time"}
-        for c in pipe:
-            c.close()
-        del host
-
+        out["e2e"] = e2e(args, work, data, params, local, Chunker, torch, np)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import chunker as och
-        from oracle import coracle
-
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        hdata = data[:sbytes].cpu().numpy()
-        p = och.Params(params.average_bits, params.seed, params.min_chunk, params.max_chunk)
-        soffs = offs[:sfiles + 1]
-        warm = min(sbytes, 1 << 20)
-        coracle.segment_files(hdata[:warm], [0, warm], p)  # load + warm
-        t0 = time.perf_counter()
-        segs, begin = coracle.segment_files(hdata, soffs, p, nthreads=threads)
-        tc = time.perf_counter() - t0
-        used = min(threads, sfiles)
-        ns1 = max(1, min(sfiles, 32))
-        if sfiles > 1:
-            t0 = time.perf_counter()
-            coracle.segment_files(hdata[:int(offs[ns1])], offs[:ns1 + 1], p, nthreads=1)
-            t1 = int(offs[ns1]) / (time.perf_counter() - t0) / GIB
-        else:
-            t1 = sbytes / tc / GIB
-        import platform
-        cpu_model = platform.processor() or ""
-        try:
-            for line in open("/proc/cpuinfo"):
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-        except OSError:
-            pass
-        what = {"c2": "the step's first configs[1] batch", "c3": "the whole stream"}.get(
-            args.config, "the shard's first files")
-        out["cpu_baseline"] = {
-            "value": round(sbytes / tc / GIB, 3), "unit": "GiB/s", "cores": used,
-            "kind": "port",
-            "sample": "%d file(s), %d B (%s) on %d thread(s), files spread over threads; "
-                      "single-thread rate from %d file(s)" % (sfiles, sbytes, what, used, ns1),
-            "single_thread_gib_s": round(t1, 4),
-            "cpu_model": cpu_model}
-        g = res.segments[:int(res.file_begin[sfiles])]
-        same = len(g) == len(segs) and all(np.array_equal(g[f], segs[f]) for f in
-                                           ("offset", "size", "file", "flags", "hash"))
-        out["parity"] = {"gpu_equals_cpu_oracle": bool(same), "segments": int(len(segs)),
-                         "checked": "the cpu_baseline sample, last measured step"}
-        if args.ref_ids:
-            nchk = min(16, len(g))
-            ok = True
-            for i in np.linspace(0, len(g) - 1, nchk).astype(int):
-                sg = g[i]
-                a = int(offs[sg["file"]]) + int(sg["offset"])
-                rid, dek = och.create_ref_id(hdata[a:a + int(sg["size"])].tobytes())
-                ok &= bytes(res.refs[i]["id"]) == rid and bytes(res.refs[i]["dek"]) == dek
-            out["parity"]["ref_ids_equal_oracle"] = bool(ok)
-            out["parity"]["ref_ids_checked"] = int(nchk)
-        if args.config == "c5" and "index" in last:
-            # the oracle's digests of the sample give the same hit rate as the GPU's
-            ref = local_index(segs, fbase)
-            out["parity"]["sample_hit_rate_gpu"] = hit_rate(last["index"][:len(ref)])
-            out["parity"]["sample_hit_rate_oracle"] = hit_rate(ref)
+        cpu_baseline(args, work, data, res, params, out, np, last)
 
     if rank == 0:
         print(json.dumps(out))
@@ -485,10 +519,234 @@ def main():
     chunker.close()
 
 
-def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, scaling, params,
-              np, torch, dist):
+def literal_batch(args, work, chunker, data, params, local, Chunker, torch):
+    """BASELINE configs[1] exactly as worded: ONE batch of 1024 x 4 MiB per step, no
+    aggregation (chain-latency bound: ~1,366 serial BLAKE2b chains fill 1/12 of the GPU)."""
+    n = args.files
+    sb = int(work.offs[n])
+    offs = work.offs[:n + 1]
+    view = data[:sb]
+    chunker.scan(view, offs)
+    torch.cuda.synchronize()
+    reps = 6
+    t0 = time.perf_counter()
+    hs = []
+    for _ in range(reps):
+        chunker.scan(view, offs)
+        hs.append(chunker.timings()["hash_span"])
+    serial = (time.perf_counter() - t0) / reps
+    # two contexts on two streams alternating (one batch each in flight)
+    other = Chunker(params, device=local)
+    pair = [chunker, other]
+    busy = [False, False]
+    other.scan(view, offs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps * 2):
+        k = i % 2
+        if busy[k]:
+            pair[k].wait()
+        pair[k].scan_async(view, offs)
+        busy[k] = True
+    for k in range(2):
+        if busy[(reps * 2 + k) % 2]:
+            pair[(reps * 2 + k) % 2].wait()
+    piped = (time.perf_counter() - t0) / (reps * 2)
+    other.close()
+    return {"value": round(sb / serial / GIB, 3), "unit": "GiB/s",
+            "ms_per_batch": round(serial * 1e3, 3),
+            "hash_span_ms_median": round(statistics.median(hs), 3),
+            "two_in_flight_value": round(sb / piped / GIB, 3),
+            "note": "one configs[1] batch (1024 x 4 MiB) per step, device-resident, no "
+                    "aggregation: bound by the ~4 MiB serial BLAKE2b chains (DESIGN.md §4)"}
+
+
+def e2e(args, work, data, params, local, Chunker, torch, np):
+    """one configs[1] batch (4 GiB) per call from pinned host memory"""
+    n = args.files
+    sbytes = int(work.offs[n])
+    host = torch.empty(sbytes, dtype=torch.uint8, pin_memory=True)
+    host.copy_(data[:sbytes])
+    hnp = host.numpy()
+    boffs = work.offs[:n + 1]
+    e2e_chunker = Chunker(params, device=local)
+    e2e_chunker.scan(hnp, boffs)
+    torch.cuda.synchronize()
+    n_e2e = 2
+    t0 = time.perf_counter()
+    for _ in range(n_e2e):
+        e2e_chunker.scan(hnp, boffs)
+    te = (time.perf_counter() - t0) / n_e2e
+    # pipelined: two contexts (two streams) alternate, so batch k+1's H2D copy runs while
+    # batch k hashes
+    pipe = [e2e_chunker, Chunker(params, device=local)]
+    pipe[1].scan(hnp, boffs)
+    n_pipe, busy = 8, [False, False]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_pipe):
+        k = i % 2
+        if busy[k]:
+            pipe[k].wait()
+        pipe[k].scan_async(hnp, boffs)
+        busy[k] = True
+    for k in range(2):
+        if busy[(n_pipe + k) % 2]:
+            pipe[(n_pipe + k) % 2].wait()
+    tp = (time.perf_counter() - t0) / n_pipe
+    for c in pipe:
+        c.close()
+    del host
+    return {"value": round(sbytes / tp / GIB, 3), "unit": "GiB/s",
+            "ms_per_batch": round(tp * 1e3, 3),
+            "serial_value": round(sbytes / te / GIB, 3),
+            "note": "configs[1] batches from pinned host memory (hipMemcpyAsync H2D + kernels "
+                    "+ records D2H), two contexts on two streams alternating so each batch's "
+                    "copy overlaps the previous batch's kernels; serial_value: one batch at a "
+                    "time"}
+
+
+def cpu_baseline(args, work, data, res, params, out, np, last):
+    """The C restatement of the reference chunker (oracle, kind "port") on the host threads
+    the box allots, over a bounded sample of the same workload, plus the parity check of the
+    GPU records on that sample."""
+    from oracle import chunker as och
+    from oracle import coracle
+
+    threads = args.cpu_threads or host_threads()
+    if args.config == "c2":
+        sfiles = min(len(work.sizes), args.files * max(1, args.cpu_batches))
+        what = "the step's first %d configs[1] batch(es)" % (sfiles // max(args.files, 1))
+    elif args.config == "c3":
+        sfiles = 1
+        what = "the whole stream (one stream: one thread)"
+    else:
+        sfiles = min(len(work.sizes), max(1, int((16 << 30) // max(work.sizes[0], 1))))
+        what = "the first %d pieces of the commit (~16 GiB)" % sfiles
+    sbytes = int(work.offs[sfiles])
+    hdata = data[:sbytes].cpu().numpy()
+    p = och.Params(params.average_bits, params.seed, params.min_chunk, params.max_chunk)
+    soffs = work.offs[:sfiles + 1]
+    warm = min(sbytes, 1 << 20)
+    coracle.segment_files(hdata[:warm], [0, warm], p)  # load + warm
+    t0 = time.perf_counter()
+    segs, begin = coracle.segment_files(hdata, soffs, p, nthreads=threads)
+    tc = time.perf_counter() - t0
+    used = min(threads, sfiles)
+    ns1 = max(1, min(sfiles, 32))
+    if sfiles > 1:
+        t0 = time.perf_counter()
+        coracle.segment_files(hdata[:int(work.offs[ns1])], work.offs[:ns1 + 1], p, nthreads=1)
+        t1 = int(work.offs[ns1]) / (time.perf_counter() - t0) / GIB
+    else:
+        t1 = sbytes / tc / GIB
+    aff = len(os.sched_getaffinity(0))
+    out["cpu_baseline"] = {
+        "value": round(sbytes / tc / GIB, 3), "unit": "GiB/s", "cores": used,
+        "kind": "port",
+        "sample": "%d file(s), %d B (%s) on %d thread(s), files spread over threads; "
+                  "single-thread rate from %d file(s)" % (sfiles, sbytes, what, used, ns1),
+        "single_thread_gib_s": round(t1, 4),
+        "host_cpus_visible": aff,
+        "threads_note": "threads = the host share the GPU box allots this job "
+                        "(OMP_NUM_THREADS); the files are independent, so the rate scales "
+                        "per thread up to the socket's cores",
+        "cpu_model": cpu_model()}
+    g = res.segments[:int(res.file_begin[sfiles])]
+    same = len(g) == len(segs) and all(np.array_equal(g[f], segs[f]) for f in
+                                       ("offset", "size", "file", "flags", "hash"))
+    out["parity"] = {"gpu_equals_cpu_oracle": bool(same), "segments": int(len(segs)),
+                     "checked": "the cpu_baseline sample, last measured step"}
+    if args.ref_ids:
+        nchk = min(16, len(g))
+        ok = True
+        for i in np.linspace(0, len(g) - 1, nchk).astype(int):
+            sg = g[i]
+            a = int(work.offs[sg["file"]]) + int(sg["offset"])
+            rid, dek = och.create_ref_id(hdata[a:a + int(sg["size"])].tobytes())
+            ok &= bytes(res.refs[i]["id"]) == rid and bytes(res.refs[i]["dek"]) == dek
+        out["parity"]["ref_ids_equal_oracle"] = bool(ok)
+        out["parity"]["ref_ids_checked"] = int(nchk)
+    if args.config == "c5" and "index" in last:
+        # the oracle's digests of the sample give the same hit rate as the GPU's
+        out["parity"]["sample_hit_rate_gpu"] = hit_rate(last["index"][:len(segs)])
+        out["parity"]["sample_hit_rate_oracle"] = hit_rate(segs)
+
+
+def bench_c3_split(args, ctx):
+    """configs[2] on N GPUs: one 10 GiB stream in equal byte ranges (strong scaling).  A step =
+    candidates of the rank's range (+64-byte halo), all-gather of the candidates, the serial
+    selection, point-to-point copies of straddling segments' bytes, BLAKE2b of the segments
+    starting in the range, all-gather of the segment records."""
+    np, torch, dist, pd = ctx["np"], ctx["torch"], ctx["dist"], ctx["pd"]
+    from pfs_amd.cdc import Chunker, SYNTH_RANDOM
+
+    world, rank, dev, cdev, params = ctx["world"], ctx["rank"], ctx["dev"], ctx["cdev"], ctx["params"]
+    seed = 0xC3 if args.seed < 0 else args.seed
+    n = C3_BYTES
+    a, b = pd.split_stream(n, world)[rank]
+    halo = min(a, 64)
+    local = torch.zeros(halo + (b - a) + params.max_chunk, dtype=torch.uint8, device=dev)
+    ch = Chunker(params, device=ctx["local"])
+    ch.fill_synthetic_pieces(local[:halo + b - a], [0, halo + b - a], [0], [a - halo], seed,
+                             SYNTH_RANDOM)
+    # collectives over RCCL on device tensors (gloo on host tensors when rehearsing)
+    cand_fn = (lambda t, h: ch.candidates(t, h))
+    hash_fn = (lambda t, bb, zz: ch.hash_ranges(t, bb, zz))
+    split = {"cand_ms": [], "hash_ms": [], "step_ms": []}
+
+    def step(record):
+        t0 = time.perf_counter()
+        segs = pd.stream_segments(local, n, (a, b), halo, params.min_chunk, params.max_chunk,
+                                  cand_fn, hash_fn, device=cdev)
+        if record:
+            tm = ch.timings()
+            split["cand_ms"].append(tm["scan"])
+            split["hash_ms"].append(tm["hash"])
+            split["step_ms"].append((time.perf_counter() - t0) * 1e3)
+        return segs
+
+    for _ in range(args.warmup):
+        step(False)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        segs = step(True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    K = max(args.steps, 1)
+    info = workload(args, world, rank).info
+    info.update({"parallelism": "stream split x%d: candidates all-gather, serial select, "
+                                "RCCL send/recv of border segments, records all-gather" % world})
+    out = {
+        "metric": "GiB/s device-resident CDC rolling-hash + chunk content-hash",
+        "value": round(n * args.steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / K, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
+        "ms_median": {k: med(v) for k, v in split.items()},
+        "index_digest": __import__("hashlib").blake2b(segs.tobytes(), digest_size=16).hexdigest(),
+        "index_segments": int(len(segs)),
+        "note": "hash_ms: this rank's segments (a split stream is bound by its longest serial "
+                "BLAKE2b chains, up to max = 20 MB)",
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    dist.destroy_process_group()
+    ch.close()
+
+
+def bench_get(args, ctx, chunker, data, work):
     """Read path: the step's segments are stored chunks (chunk.Create form); one step =
     pfscdc_get_chunks over all of them (verify + decrypt, device in/out)."""
+    np, torch, dist = ctx["np"], ctx["torch"], ctx["dist"]
+    world, rank, cdev = ctx["world"], ctx["rank"], ctx["cdev"]
+    total, offs = work.total, work.offs
     chunker.set_ref_ids(True)
     res = chunker.scan(data, offs)  # segments + Ref (id, dek): the chunks as stored
     segs = res.segments
@@ -504,11 +762,11 @@ def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, s
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kms = 0.0
+    kms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         _, ok = chunker.get_chunks(ctext, cofs, res.refs, out=out)
-        kms += chunker.last_get_ms()
+        kms.append(chunker.last_get_ms())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -516,15 +774,16 @@ def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, s
     same = bool(ok.all()) and bool(torch.equal(out, data))
     bytes_step = total
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        bt = torch.tensor([total], dtype=torch.float64, device=cdev)
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_step = int(bt.item())
     K = max(args.steps, 1)
-    ms = kms / K
+    ms = sum(kms) / len(kms) if kms else 0.0
     ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    info = dict(work.info)
     info.update({"path": "get (chunk.Get: verify Ref.Id, ChaCha20 decrypt)",
                  "chunks_per_step": int(len(segs))})
     out_line = {
@@ -532,9 +791,9 @@ def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, s
         "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "scaling": work.scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic plaintext encrypted on the GPU with its own Ref.Dek", "config": info,
-        "kernel_ms": {"get": round(ms, 4)},
+        "kernel_ms": {"get": round(ms, 4)}, "kernel_ms_median": {"get": med(kms)},
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
@@ -549,38 +808,22 @@ def bench_get(args, world, rank, local, dev, chunker, data, offs, total, info, s
 
 
 def commit_layout(sizes, mem_threshold):
-    """UnorderedWriter.Put of the files in path order (unordered_writer.go:45-72): the files
-    cut into pieces at every mem_threshold bytes, each run of pieces one serialized fileset.
-    A Put that fills the threshold exactly re-Adds its path empty in the next fileset.
-    Returns (piece sizes, stream_file_begin over pieces)."""
-    pieces, streams = [], [0]
-    avail = mem_threshold
-    for n in sizes:
-        n, pos = int(n), 0
-        pieces.append(0)  # buffer.Add(p, tag)
-        while True:  # io.CopyN(w, r, memAvailable)
-            got = min(avail, n - pos)
-            pieces[-1] += got
-            pos += got
-            eof = got < avail
-            avail -= got
-            if eof:
-                break
-            if avail == 0:  # serialize, then re-Add the same path
-                streams.append(len(pieces))
-                avail = mem_threshold
-                pieces.append(0)
-    if streams[-1] != len(pieces):  # Close serializes the rest
-        streams.append(len(pieces))
-    return pieces, streams
+    """(piece sizes, fileset begin indices over pieces) of UnorderedWriter.Put of the files in
+    path order: pfs_amd.distributed.commit_layout (unordered_writer.go:45-72)."""
+    from pfs_amd import distributed as pd
+    lay = pd.commit_layout(sizes, mem_threshold)
+    return [int(x) for x in lay.size], [int(x) for x in lay.fileset_begin]
 
 
-def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, scaling, params,
-                 np, torch, dist):
+def bench_commit(args, ctx):
     """pachd data plane on the step's files: pieces / filesets (commit_layout), CDC + DataRef
     hashes (one scan of all pieces), chunk formation per fileset stream (pfscdc_form_chunks),
     chunk.Create of every formed chunk (pfscdc_create_refs: content hash of multi-DataRef
     chunks, dek, ChaCha20 + BLAKE2b of the ciphertext).
+
+    N>1: whole serialized filesets per rank (a fresh chunk.Writer per fileset, so chunks never
+    span ranks); each rank forms its chunks and Refs, and the chunk records (offset in the
+    commit stream, size, Ref.Id, Ref.Dek) are all-gathered: the same list as N=1.
 
     With --inflight S > 1, S contexts (S HIP streams) each run every S-th step from their own
     host thread, so one step's chunk.Create tail (the serial BLAKE2b chains of its largest
@@ -588,17 +831,36 @@ def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, sca
     read the same device buffer (the same files committed again; the library only reads it)."""
     import threading
 
-    S = len(chunkers)
-    pieces, streams = commit_layout(sizes, args.mem_threshold)
-    poffs = np.zeros(len(pieces) + 1, dtype=np.uint64)
-    poffs[1:] = np.cumsum(np.asarray(pieces, dtype=np.uint64))
-    assert int(poffs[-1]) == total
+    np, torch, dist, pd = ctx["np"], ctx["torch"], ctx["dist"], ctx["pd"]
+    world, rank, dev, cdev, params = ctx["world"], ctx["rank"], ctx["dev"], ctx["cdev"], ctx["params"]
+    from pfs_amd.cdc import Chunker
+
+    args.group = 1
+    work = workload(args, world, rank) if args.config in ("c4", "c5") else None
+    if work is None:  # c2/c3 files committed as one commit: pieces per fileset
+        base = workload(args, 1, 0)
+        lay = pd.commit_layout(base.sizes, args.mem_threshold)
+        fs = pd.shard_filesets(lay, world)[rank]
+        p0, p1 = pd.rank_pieces(lay, fs)
+        ids = base.ids[lay.file[p0:p1]]
+        starts = base.starts[lay.file[p0:p1]] + lay.start[p0:p1]
+        work = Work(lay.size[p0:p1], ids, starts, base.seed, base.mode, base.info, "strong",
+                    gbase=p0)
+        work.layout, work.fs_range = lay, fs
+    lay, fs = work.layout, work.fs_range
+    p0 = work.gbase
+    streams = (lay.fileset_begin[fs[0]:fs[1] + 1] - p0).astype(np.uint32)
+    total = work.total
+    S = args.inflight if args.inflight > 0 else 1
+    data = torch.empty(total, dtype=torch.uint8, device=dev)
+    chunkers = [Chunker(params, device=ctx["local"]) for _ in range(S)]
+    fill(chunkers[0], data, work)
+    poffs = work.offs
+    gbyte = int(lay.offsets()[p0])  # this rank's first byte in the commit stream
     keys = ("scan", "hash", "total", "create", "create_content_hash", "create_ref_id",
             "host_form_ms")
     accs = [dict.fromkeys(keys, 0.0) for _ in range(S)]
     lasts = [{} for _ in range(S)]
-    for ch in chunkers:
-        ch.set_ref_ids(False)
 
     def step(k, record):
         chunker, acc = chunkers[k], accs[k]
@@ -658,10 +920,10 @@ def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, sca
     elapsed = time.perf_counter() - t0
     bytes_step = total
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        bt = torch.tensor([total], dtype=torch.float64, device=dev)
+        bt = torch.tensor([total], dtype=torch.float64, device=cdev)
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_step = int(bt.item())
     K = max(args.steps, 1)
@@ -669,22 +931,36 @@ def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, sca
     last = lasts[0]
     coffs, known = last["coffs"], last["known"]
     nch = len(coffs) - 1
+    # the commit's chunk list: (offset in the commit stream, size, Ref.Id, Ref.Dek) per chunk
+    cdt = np.dtype([("offset", "<u8"), ("size", "<u8"), ("id", "u1", (32,)), ("dek", "u1", (32,))])
+    crec = np.zeros(nch, dtype=cdt)
+    crec["offset"] = coffs[:-1] + np.uint64(gbyte)
+    crec["size"] = np.diff(coffs)
+    crec["id"] = last["refs"]["id"]
+    crec["dek"] = last["refs"]["dek"]
+    chunks = pd.gather_records(crec, device=cdev) if world > 1 else crec
+    info = dict(work.info)
     info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
                          "chunk.Create)", "mem_threshold": args.mem_threshold,
-                 "filesets_per_step": len(streams) - 1, "pieces_per_step": len(pieces),
-                 "chunks_per_step": nch, "multi_dataref_chunks": int(nch - int(known.sum())),
-                 "steps_in_flight": S})
+                 "filesets_this_rank": fs[1] - fs[0], "pieces_this_rank": len(work.sizes),
+                 "chunks_this_rank": nch, "chunks_per_commit": int(len(chunks)),
+                 "multi_dataref_chunks": int(nch - int(known.sum())),
+                 "steps_in_flight": S,
+                 "parallelism": "fileset-sharded x%d, all-gather of the chunk records" % world
+                 if world > 1 else "single GPU"})
     ms = avg["create"]
     ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    import hashlib
     out = {
         "metric": "GiB/s device-resident pachd commit data plane (CDC + DataRef hashes + "
                   "chunk formation + chunk.Create Ref.Id)",
         "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
         "kernel_ms": {name: round(v, 4) for name, v in avg.items()},
+        "commit_chunks_digest": hashlib.blake2b(chunks.tobytes(), digest_size=16).hexdigest(),
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
@@ -694,7 +970,7 @@ def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, sca
         out["note"] = ("kernel_ms are per step on its own stream; with %d steps in flight they "
                        "overlap, so ms_per_step < their sum" % S)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["parity"] = commit_parity(data, pieces, streams, poffs, last, params, np)
+        out["parity"] = commit_parity(data, work, streams, last, params, np)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
@@ -703,35 +979,51 @@ def bench_commit(args, world, rank, dev, chunkers, data, sizes, total, info, sca
         ch.close()
 
 
-def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params, np, torch,
-             dist):
-    """Host-fed pachd write path: the step's first --uw-bytes of files (host memory) Put
+def bench_uw(args, ctx):
+    """Host-fed pachd write path: the first --uw-bytes of the commit's files (host memory) Put
     through the UnorderedWriter (pfs_amd.fileset over pfscdc_uw_*): buffering, 1e9-byte
-    filesets, GPU chunk writers with Ref ids and ciphertext upload off, index writers."""
+    filesets, GPU chunk writers with Ref ids, index writers.  N>1: whole serialized filesets
+    per rank (each rank its own UnorderedWriter over its pieces, the re-Added continuation of
+    a split file Put with append); the filesets (SizeBytes, root indexes) are all-gathered:
+    the same list as one writer's."""
+    np, torch, dist, pd = ctx["np"], ctx["torch"], ctx["dist"], ctx["pd"]
+    world, rank, dev, cdev, params = ctx["world"], ctx["rank"], ctx["dev"], ctx["cdev"], ctx["params"]
     from pfs_amd import fileset as pf
+    from pfs_amd.cdc import Chunker
 
+    base = workload(args, 1, 0) if args.config in ("c2", "c3") else None
+    if base is None:
+        sizes = [C4_FILE_BYTES] * C4_FILES
+        sizes[-1] += C4_TAIL
+        seed = (0xC4 if args.config == "c4" else 0xC5) if args.seed < 0 else args.seed
+        mode = workload(args, 1, 0).mode if args.config == "c5" else 0
+    else:
+        sizes, seed, mode = base.sizes, base.seed, base.mode
     offs = np.zeros(len(sizes) + 1, dtype=np.uint64)
     offs[1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
-    nf = int(np.searchsorted(offs, min(args.uw_bytes, int(offs[-1])), side="right")) - 1
-    nf = max(1, nf)
-    nbytes = int(offs[nf])
-    host = data[:nbytes].cpu().numpy()
-    views = [memoryview(host[int(offs[f]):int(offs[f + 1])]) for f in range(nf)]
-    chunker.close()
-    st = pf.Storage(rank % max(1, torch.cuda.device_count()), params, args.mem_threshold)
+    nf = max(1, int(np.searchsorted(offs, min(args.uw_bytes, int(offs[-1])), side="right")) - 1)
+    lay = pd.commit_layout(sizes[:nf], args.mem_threshold)
+    fs = pd.shard_filesets(lay, world)[rank]
+    p0, p1 = pd.rank_pieces(lay, fs)
+    pieces = Work(lay.size[p0:p1], lay.file[p0:p1], lay.start[p0:p1], seed, mode, {}, "strong")
+    nbytes = pieces.total
+    gen = Chunker(params, device=ctx["local"])
+    t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    fill(gen, t, pieces)
+    host = t[:nbytes].cpu().numpy()
+    gen.close()
+    del t
+    torch.cuda.empty_cache()
+    views = {}  # (file, start) -> the piece's bytes in host memory
+    for i in range(p0, p1):
+        o = int(pieces.offs[i - p0])
+        views[(int(lay.file[i]), int(lay.start[i]))] = memoryview(host[o:o + int(lay.size[i])])
+    st = pf.Storage(ctx["local"], params, args.mem_threshold)
 
-    split = {"put_ms": 0.0, "close_ms": 0.0}
-
-    def step(record=False):
+    def step():
         w = st.new_unordered_writer()
-        t0 = time.perf_counter()
-        for f in range(nf):
-            w.put("/%016d" % f, "", False, views[f])
-        t1 = time.perf_counter()
-        prims = w.close()
-        if record:
-            split["put_ms"] += (t1 - t0) * 1e3
-            split["close_ms"] += (time.perf_counter() - t1) * 1e3
+        prims = pd.put_rank_filesets(w, lay, fs, lambda f: "/%016d" % f,
+                                     lambda f, s, n: views[(f, s)])
         return prims, w
 
     for _ in range(args.warmup):
@@ -740,33 +1032,41 @@ def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        prims, w = step(True)
+        prims, w = step()
     elapsed = time.perf_counter() - t0
     bytes_step = nbytes
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        bt = torch.tensor([nbytes], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        bt = torch.tensor([nbytes], dtype=torch.float64, device=cdev)
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_step = int(bt.item())
+    gathered = pd.gather_primitives(prims, device=cdev) if world > 1 else \
+        [(p.additive, p.deletive, p.size_bytes) for p in prims]
+    import hashlib
     K = max(args.steps, 1)
-    nchunks = sum(1 for fs in w.events for e in fs if e[0] == "chunk" and e[1] == -1)
-    info.update({"path": "uw (host-fed UnorderedWriter -> fileset.Writer -> index.Writer)",
-                 "files_per_step": nf, "bytes_per_step": nbytes,
-                 "mem_threshold": args.mem_threshold, "filesets_per_step": len(prims),
-                 "data_chunks_per_step": nchunks})
+    nchunks = sum(1 for fsv in w.events for e in fsv if e[0] == "chunk" and e[1] == -1)
+    info = {"workload": "the first %d files (%d B) of %s, Put from host memory" % (
+                nf, int(offs[nf]), args.config),
+            "path": "uw (host-fed UnorderedWriter -> fileset.Writer -> index.Writer)",
+            "bytes_this_rank": nbytes, "mem_threshold": args.mem_threshold,
+            "filesets": lay.nfilesets, "filesets_this_rank": len(prims),
+            "data_chunks_this_rank": nchunks,
+            "parallelism": "fileset-sharded x%d, all-gather of the fileset roots" % world
+            if world > 1 else "single GPU"}
     out = {
         "metric": "GiB/s host-fed pachd write path (Put -> filesets with chunk Refs and "
                   "multilevel indexes)",
         "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic bytes in host memory", "config": info,
-        "split_ms": {k: round(v / K, 1) for k, v in split.items()},
-        "note": "put_ms: the Put loop (one host copy into the fileset arenas, serializations "
-                "deferred); close_ms: the grouped GPU write of every fileset plus the indexes",
+        "commit_filesets_digest": hashlib.blake2b(
+            b"".join(pd.encode_primitive(*g) for g in gathered), digest_size=16).hexdigest(),
+        "note": "a step: the Puts (one host copy into the fileset arenas) and the grouped "
+                "GPU write of every fileset plus the indexes, then Close",
     }
     if rank == 0:
         print(json.dumps(out))
@@ -774,18 +1074,24 @@ def bench_uw(args, world, rank, dev, chunker, data, sizes, info, scaling, params
         dist.destroy_process_group()
 
 
-def bench_rechunk(args, world, rank, dev, chunker, data, info, scaling, params, np, torch,
-                  dist):
-    """Re-chunk path (MergeFileReader.Hash, the Writer.Copy machinery): the step's first
-    1 GiB as one file written by --rechunk-writers writers (each its own chunk stream,
-    ciphertexts uploaded to the in-memory store), then the merged file's hash: Copy of every
-    DataRef through a fresh writer, whole aligned chunks passed through, the rest read back
-    (chunk.Get on the GPU) and re-rolled.  Checked against the single-writer hash."""
+def bench_rechunk(args, ctx):
+    """Re-chunk path (MergeFileReader.Hash, the Writer.Copy machinery): a 1 GiB file written
+    by --rechunk-writers writers (each its own chunk stream, ciphertexts uploaded to the
+    in-memory store), then the merged file's hash: Copy of every DataRef through a fresh
+    writer, whole aligned chunks passed through, the rest read back (chunk.Get on the GPU) and
+    re-rolled.  Checked against the single-writer hash."""
+    np, torch, dev = ctx["np"], ctx["torch"], ctx["dev"]
+    world = ctx["world"]
     from pfs_amd import chunk as pc
+    from pfs_amd.cdc import Chunker, SYNTH_RANDOM
 
-    nbytes = min(1 << 30, data.numel())
-    host = data[:nbytes].cpu().numpy()
-    chunker.close()
+    nbytes = 1 << 30
+    gen = Chunker(ctx["params"], device=ctx["local"])
+    t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    gen.fill_synthetic(t, [0, nbytes], 0xC2 if args.seed < 0 else args.seed, SYNTH_RANDOM)
+    host = t.cpu().numpy()
+    gen.close()
+    del t
     store = pc.ChunkStore()
     st = pc.Storage(dev.index or 0, store=store)
 
@@ -814,32 +1120,33 @@ def bench_rechunk(args, world, rank, dev, chunker, data, info, scaling, params, 
     elapsed = time.perf_counter() - t0
     K = max(args.steps, 1)
     edge = sum(1 for d in refs if d.ref.edge)
-    info.update({"path": "rechunk (MergeFileReader.Hash of a file written by %d writers)" % k,
-                 "file_bytes": nbytes, "data_refs": len(refs), "edge_data_refs": edge,
-                 "store_chunks": len(store)})
+    info = {"path": "rechunk (MergeFileReader.Hash of a file written by %d writers)" % k,
+            "file_bytes": nbytes, "data_refs": len(refs), "edge_data_refs": edge,
+            "store_chunks": len(store)}
     out = {
         "metric": "GiB/s of file bytes through MergeFileReader.Hash (Writer.Copy re-chunking)",
         "value": round(nbytes * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM, copied to host)",
         "config": info,
         "parity": {"merged_hash_equals_single_writer_hash": got == want},
     }
-    if rank == 0:
+    if ctx["rank"] == 0:
         print(json.dumps(out))
     if world > 1:
-        dist.destroy_process_group()
+        ctx["dist"].destroy_process_group()
 
 
-def commit_parity(data, pieces, streams, poffs, last, params, np):
+def commit_parity(data, work, streams, last, params, np):
     """The first fileset through the CPU oracle: segments (C restatement), the chunk.Writer
     replay (oracle.chunker), and chunk.Create of a sample of its chunks."""
     from oracle import chunker as och
     from oracle import coracle
 
-    f1 = streams[1]
+    poffs = work.offs
+    f1 = int(streams[1])
     nb = int(poffs[f1])
     host = data[:nb].cpu().numpy()
     p = och.Params(params.average_bits, params.seed, params.min_chunk, params.max_chunk)

@@ -167,7 +167,7 @@ int pfscdc_last_create_timings(pfscdc_ctx* ctx, float out[2]);
  * stream start, where positions < 63 are never candidates: min >= 64 puts them before the
  * first eligible cut).  out: cap entries; *n = the count (PFSCDC_ENOMEM if > cap, out holds
  * the first cap).  Tiles with more than 15 candidates are re-rolled exactly on the host.
- * Timings: pfscdc_last_timings out[0] (scan) and out[1] (compaction). */
+ * Timings: pfscdc_last_timings out[0] (scan, compaction included). */
 int pfscdc_candidates(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                       uint64_t halo, uint64_t* out, uint64_t cap, uint64_t* n);
 
@@ -183,8 +183,17 @@ int pfscdc_hash_ranges(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
 uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
 
 /* Device timing of the last scan's kernels (ms, HIP events on the ctx stream):
- * out[0] candidate scan, out[1] compaction, out[2] selection, out[3] BLAKE2b, out[4] total. */
+ * out[0] candidate scan (its last workgroup also compacts the candidates), out[1] 0 (the
+ * compaction used to be a launch of its own), out[2] selection (its last workgroup also
+ * compacts the segment list and builds the hash queue's LPT order), out[3] BLAKE2b,
+ * out[4] total.  An interval between two events includes any time the kernel waited for
+ * free CUs behind work of another stream. */
 int pfscdc_last_timings(pfscdc_ctx* ctx, float out[5]);
+/* Execution spans of the last scan's two main kernels (ms): out[0] the candidate scan, out[1]
+ * the BLAKE2b kernel, each from its first wavefront's start to its last wavefront's end
+ * (s_memrealtime in the kernels), so a kernel queued behind another stream's work is not
+ * charged for the wait — the per-launch duration a kernel-trace profiler reports. */
+int pfscdc_last_kernel_spans(pfscdc_ctx* ctx, float out[2]);
 
 /* Pinned host memory for staging (PCIe-inclusive end-to-end path). */
 void* pfscdc_host_alloc(uint64_t nbytes);

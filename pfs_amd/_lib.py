@@ -45,6 +45,7 @@ EXPORTED = [
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
     "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
+    "pfscdc_last_kernel_spans",
 ]
 
 
@@ -174,6 +175,7 @@ def load() -> C.CDLL:
             "pfscdc_file_segment_begin": (P(u64), [vp]),
             "pfscdc_debug_candidates": (u64, [vp, P(u64), u64]),
             "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
+            "pfscdc_last_kernel_spans": (i32, [vp, P(C.c_float)]),
             "pfscdc_set_options": (i32, [vp, u32]),
             "pfscdc_refs": (vp, [vp]),
             "pfscdc_last_ref_ms": (i32, [vp, P(C.c_float)]),

@@ -156,6 +156,9 @@ class Chunker:
         out = (C.c_float * 5)()
         self._check(self.lib.pfscdc_last_timings(self.ctx, out), "timings")
         t = dict(zip(["scan", "compact", "select", "hash", "total"], list(out)))
+        sp = (C.c_float * 2)()
+        self._check(self.lib.pfscdc_last_kernel_spans(self.ctx, sp), "kernel_spans")
+        t["scan_span"], t["hash_span"] = sp[0], sp[1]
         if self.ref_ids:
             ms = C.c_float()
             self._check(self.lib.pfscdc_last_ref_ms(self.ctx, C.byref(ms)), "timings")

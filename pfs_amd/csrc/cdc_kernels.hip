@@ -333,11 +333,29 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
 // swz(r) = (r >> 1) & 7, so the row reads (ds_read_b128) are bank-conflict free.
 PFS_DEV uint32_t stage_swz(uint32_t r) { return (r >> 1) & 7u; }
 
+template <int BLOCK>
+PFS_DEV void compact_tiles(const TileRec* __restrict__ recs, uint64_t ntiles, uint64_t n,
+                           uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries,
+                           uint64_t* s_wave);
+PFS_DEV bool last_block_done(uint32_t* done_ctr, uint32_t* s_flag);
+
+// Exact kernel execution span for timing (bench roofline): the first wavefront to start
+// lowers span[0], the last to finish raises span[1] (s_memrealtime, the constant wall clock;
+// vector atomics).  span == nullptr: not recorded.
+PFS_DEV void span_begin(uint64_t* span) {
+  if (span && threadIdx.x == 0) atomicMin((unsigned long long*)span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+PFS_DEV void span_end(uint64_t* span) {
+  if (span && (threadIdx.x & 63) == 0) atomicMax((unsigned long long*)span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 template <bool WIDE>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
-    TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr) {
+    TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr, uint32_t* __restrict__ done_ctr,
+    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries, uint64_t* span) {
+  span_begin(span);
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
   // images.  recs[] is zeroed before the launch; candidates are added to it directly.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -457,14 +475,25 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
       }
     }
   }
+  // the last workgroup compacts the tile records into the sorted entry list (the table and
+  // staging LDS are free once every wave of the workgroup is past its last unit)
+  if (done_ctr) {
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(smem);
+    uint64_t* s_wave = reinterpret_cast<uint64_t*>(smem + 64);
+    if (last_block_done(done_ctr, s_flag))
+      compact_tiles<kScanBlock>(recs, ntiles, n, entries, n_entries, s_wave);
+  }
+  span_end(span);
 }
 
 // ------------------------------------------------------------------------------------------
 // 2. compaction: tile records -> sorted entry list
 // ------------------------------------------------------------------------------------------
 
-// Block-wide exclusive scan (1024 threads = 16 waves); returns exclusive prefix, *total set.
-PFS_DEV uint64_t block_exclusive_scan(uint64_t v, uint64_t* s_wave, uint64_t* total) {
+// Block-wide exclusive scan (BLOCK threads, BLOCK/64 waves, s_wave[BLOCK/64 + 1] of LDS);
+// returns the exclusive prefix and sets *total.
+template <int BLOCK>
+PFS_DEV uint64_t block_exscan(uint64_t v, uint64_t* s_wave, uint64_t* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t x = v;
 #pragma unroll
@@ -477,26 +506,43 @@ PFS_DEV uint64_t block_exclusive_scan(uint64_t v, uint64_t* s_wave, uint64_t* to
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t run = 0;
-    for (int w = 0; w < kCompactBlock / 64; w++) {
+    for (int w = 0; w < BLOCK / 64; w++) {
       const uint64_t t = s_wave[w];
       s_wave[w] = run;
       run += t;
     }
-    s_wave[kCompactBlock / 64] = run;
+    s_wave[BLOCK / 64] = run;
   }
   __syncthreads();
   const uint64_t r = s_wave[wave] + x - v;
-  *total = s_wave[kCompactBlock / 64];
+  *total = s_wave[BLOCK / 64];
   __syncthreads();
   return r;
 }
 
-__global__ __launch_bounds__(kCompactBlock) void compact_kernel(
-    const TileRec* __restrict__ recs, uint64_t ntiles, uint64_t n,
-    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries) {
-  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+// "Last workgroup" hand-off for the small serial steps of the pipeline (compaction after
+// the scan; segment compaction and the LPT order after the selection): every workgroup
+// writes back its stores (device-scope release: buffer_wbl2 on each XCD's L2) and counts
+// itself done; the one that counts last acquires (buffer_inv) and runs the step itself.  A
+// separate one-workgroup launch would instead wait for a whole free CU behind the other
+// step's resident hash waves (15 ms instead of 0.2 ms with two steps in flight).
+PFS_DEV bool last_block_done(uint32_t* done_ctr, uint32_t* s_flag) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) *s_flag = atomicAdd(done_ctr, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  const bool last = *s_flag != 0;
+  if (last) __threadfence();
+  return last;
+}
+
+// Tile records -> sorted entry list (the scan's candidates in stream order).
+template <int BLOCK>
+PFS_DEV void compact_tiles(const TileRec* __restrict__ recs, uint64_t ntiles, uint64_t n,
+                           uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries,
+                           uint64_t* s_wave) {
   uint64_t carry = 0;
-  for (uint64_t base = 0; base < ntiles; base += kCompactBlock) {
+  for (uint64_t base = 0; base < ntiles; base += BLOCK) {
     const uint64_t t = base + threadIdx.x;
     uint32_t c = 0;
     uint64_t e = 0;
@@ -505,7 +551,7 @@ __global__ __launch_bounds__(kCompactBlock) void compact_kernel(
       e = c <= (uint32_t)kTileK ? c : 1;
     }
     uint64_t total;
-    const uint64_t ex = block_exclusive_scan(e, s_wave, &total) + carry;
+    const uint64_t ex = block_exscan<BLOCK>(e, s_wave, &total) + carry;
     if (t < ntiles) {
       const uint64_t ts = t * kTile;
       if (c <= (uint32_t)kTileK) {
@@ -528,6 +574,74 @@ __global__ __launch_bounds__(kCompactBlock) void compact_kernel(
     carry += total;
   }
   if (threadIdx.x == 0) *n_entries = carry;
+}
+
+__global__ __launch_bounds__(kCompactBlock) void compact_kernel(
+    const TileRec* __restrict__ recs, uint64_t ntiles, uint64_t n,
+    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries) {
+  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+  compact_tiles<kCompactBlock>(recs, ntiles, n, entries, n_entries, s_wave);
+}
+
+// Per-file segment counts -> dense segment list in (file, offset) order; returns the total.
+template <int BLOCK>
+PFS_DEV uint64_t segcompact_block(const pfscdc_segment* __restrict__ slots,
+                                  const uint64_t* __restrict__ seg_base,
+                                  const uint64_t* __restrict__ nseg, uint32_t nfiles,
+                                  pfscdc_segment* __restrict__ segs,
+                                  uint64_t* __restrict__ seg_begin, uint64_t* s_wave) {
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < nfiles; base += BLOCK) {
+    const uint64_t f = base + threadIdx.x;
+    const uint64_t c = f < nfiles ? nseg[f] : 0;
+    uint64_t total;
+    const uint64_t ex = block_exscan<BLOCK>(c, s_wave, &total) + carry;
+    if (f < nfiles) {
+      seg_begin[f] = ex;
+      const pfscdc_segment* src = slots + seg_base[f];
+      for (uint64_t i = 0; i < c; i++) segs[ex + i] = src[i];
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) seg_begin[nfiles] = carry;
+  return carry;
+}
+
+// LPT order: segment indices sorted by block count, longest first (counting sort on a 10-bit
+// key).  The hash kernel's quads pull segments in this order, so the longest serial chains
+// start first and the short ones fill in behind them.
+PFS_DEV uint32_t lpt_key(uint64_t size) {
+  const uint64_t nblk = (size + 127) / 128;
+  const uint64_t k = nblk >> 6;  // 8 KiB granularity
+  return 1023u - (uint32_t)(k < 1023 ? k : 1023);  // ascending key = descending length
+}
+
+template <int BLOCK>
+PFS_DEV void lpt_order_block(const pfscdc_segment* __restrict__ segs, uint64_t n,
+                             uint32_t* __restrict__ order, uint32_t* __restrict__ counter,
+                             uint32_t* hist, uint64_t* s_wave) {
+  constexpr int kPer = 1024 / BLOCK;  // histogram bins per thread
+  static_assert(1024 % BLOCK == 0, "bins split evenly over the block");
+  for (int b = 0; b < kPer; b++) hist[threadIdx.x * kPer + b] = 0;
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&hist[lpt_key(segs[i].size)], 1u);
+  __syncthreads();
+  uint32_t local[kPer];
+  uint64_t sum = 0;
+  for (int b = 0; b < kPer; b++) {
+    local[b] = hist[threadIdx.x * kPer + b];
+    sum += local[b];
+  }
+  uint64_t total;
+  uint64_t start = block_exscan<BLOCK>(sum, s_wave, &total);
+  for (int b = 0; b < kPer; b++) {
+    hist[threadIdx.x * kPer + b] = (uint32_t)start;
+    start += local[b];
+  }
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < n; i += BLOCK)
+    order[atomicAdd(&hist[lpt_key(segs[i].size)], 1u)] = (uint32_t)i;
+  if (threadIdx.x == 0) *counter = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -558,14 +672,12 @@ PFS_DEV uint64_t rescan_first(const uint8_t* __restrict__ data, const uint64_t* 
   return kNone;
 }
 
-__global__ __launch_bounds__(kSelectBlock) void select_kernel(
+PFS_DEV void select_file(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ T,
     const uint64_t* __restrict__ entries, const uint64_t* __restrict__ n_entries,
-    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ seg_base, uint32_t nfiles,
+    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ seg_base, uint64_t f,
     uint64_t mask, uint64_t min_chunk, uint64_t max_chunk,
     pfscdc_segment* __restrict__ slots, uint64_t* __restrict__ nseg) {
-  const uint64_t f = ((uint64_t)blockIdx.x * kSelectBlock + threadIdx.x) >> 6;
-  if (f >= nfiles) return;  // wave-uniform
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t fs = offs[f], fe = offs[f + 1];
   const uint64_t sb = seg_base[f], cap = seg_base[f + 1] - sb;
@@ -631,8 +743,35 @@ __global__ __launch_bounds__(kSelectBlock) void select_kernel(
   }
 }
 
+// One wave per file; the last workgroup to finish then compacts the per-file segment slots
+// into the dense (file, offset)-ordered list and builds the hash queue's LPT order (both
+// once per batch, see last_block_done).
+__global__ __launch_bounds__(kSelectBlock) void select_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ T,
+    const uint64_t* __restrict__ entries, const uint64_t* __restrict__ n_entries,
+    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ seg_base, uint32_t nfiles,
+    uint64_t mask, uint64_t min_chunk, uint64_t max_chunk,
+    pfscdc_segment* __restrict__ slots, uint64_t* __restrict__ nseg, uint32_t* done_ctr,
+    pfscdc_segment* __restrict__ segs, uint64_t* __restrict__ seg_begin,
+    uint32_t* __restrict__ order, uint32_t* __restrict__ counter) {
+  __shared__ uint32_t hist[1024];
+  __shared__ uint64_t s_wave[kSelectBlock / 64 + 1];
+  __shared__ uint32_t s_flag;
+  const uint64_t f = ((uint64_t)blockIdx.x * kSelectBlock + threadIdx.x) >> 6;
+  if (f < nfiles)  // wave-uniform
+    select_file(data, T, entries, n_entries, offs, seg_base, f, mask, min_chunk, max_chunk,
+                slots, nseg);
+  if (!last_block_done(done_ctr, &s_flag)) return;
+  const uint64_t total = segcompact_block<kSelectBlock>(slots, seg_base, nseg, nfiles, segs,
+                                                        seg_begin, s_wave);
+  __threadfence_block();
+  __syncthreads();
+  if (order) lpt_order_block<kSelectBlock>(segs, total, order, counter, hist, s_wave);
+}
+
 // ------------------------------------------------------------------------------------------
-// 4. segment compaction (per-file counts -> dense list in (file, offset) order)
+// 4. segment compaction (per-file counts -> dense list in (file, offset) order) and the LPT
+//    order of the hash queue
 // ------------------------------------------------------------------------------------------
 
 __global__ __launch_bounds__(kCompactBlock) void segcompact_kernel(
@@ -640,20 +779,15 @@ __global__ __launch_bounds__(kCompactBlock) void segcompact_kernel(
     const uint64_t* __restrict__ nseg, uint32_t nfiles, pfscdc_segment* __restrict__ segs,
     uint64_t* __restrict__ seg_begin) {
   __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
-  uint64_t carry = 0;
-  for (uint64_t base = 0; base < nfiles; base += kCompactBlock) {
-    const uint64_t f = base + threadIdx.x;
-    const uint64_t c = f < nfiles ? nseg[f] : 0;
-    uint64_t total;
-    const uint64_t ex = block_exclusive_scan(c, s_wave, &total) + carry;
-    if (f < nfiles) {
-      seg_begin[f] = ex;
-      const pfscdc_segment* src = slots + seg_base[f];
-      for (uint64_t i = 0; i < c; i++) segs[ex + i] = src[i];
-    }
-    carry += total;
-  }
-  if (threadIdx.x == 0) seg_begin[nfiles] = carry;
+  segcompact_block<kCompactBlock>(slots, seg_base, nseg, nfiles, segs, seg_begin, s_wave);
+}
+
+__global__ __launch_bounds__(kCompactBlock) void hash_order_kernel(
+    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
+    uint32_t* __restrict__ order, uint32_t* __restrict__ counter) {
+  __shared__ uint32_t hist[1024];
+  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
+  lpt_order_block<kCompactBlock>(segs, *seg_count, order, counter, hist, s_wave);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -768,34 +902,8 @@ PFS_DEV void msg_load_tail(uint4& m0, uint4& m1, const uint8_t* p, int64_t avail
   m1 = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-// 5a. LPT order: segment indices sorted by block count, longest first (counting sort on a
-// 10-bit key, one workgroup).  The hash kernel's quads pull segments in this order, so the
-// longest serial chains start first and the short ones fill in behind them.
-PFS_DEV uint32_t lpt_key(uint64_t size) {
-  const uint64_t nblk = (size + 127) / 128;
-  const uint64_t k = nblk >> 6;  // 8 KiB granularity
-  return 1023u - (uint32_t)(k < 1023 ? k : 1023);  // ascending key = descending length
-}
-
-__global__ __launch_bounds__(kCompactBlock) void hash_order_kernel(
-    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
-    uint32_t* __restrict__ order, uint32_t* __restrict__ counter) {
-  static_assert(kCompactBlock == 1024, "one histogram bin per thread");
-  __shared__ uint32_t hist[1024];
-  __shared__ uint64_t s_wave[kCompactBlock / 64 + 1];
-  const uint64_t n = *seg_count;
-  hist[threadIdx.x] = 0;
-  __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n; i += kCompactBlock) atomicAdd(&hist[lpt_key(segs[i].size)], 1u);
-  __syncthreads();
-  uint64_t total;
-  const uint64_t start = block_exclusive_scan(hist[threadIdx.x], s_wave, &total);
-  hist[threadIdx.x] = (uint32_t)start;
-  __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n; i += kCompactBlock)
-    order[atomicAdd(&hist[lpt_key(segs[i].size)], 1u)] = (uint32_t)i;
-  if (threadIdx.x == 0) *counter = 0;
-}
+// 5a. LPT order: see lpt_order_block (run by the last selection workgroup, or alone by
+// hash_order_kernel for the chunk.Create / chunk.Get passes).
 
 // 5b. BLAKE2b-256 per segment: 4 lanes (a quad) hash one segment, lane j owning column j of
 // the 4x4 state; waves stay resident and each quad pulls its next segment from the LPT
@@ -960,8 +1068,10 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
-    pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks) {
+    pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks,
+    uint64_t* span) {
   constexpr bool CIPHER = MODE != kModeHash;
+  span_begin(span);
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
   // i&1 while the quad's next block (loaded into registers one iteration earlier) is written
   // to the other buffer halfway through; the wave-uniform parity makes every ds_read offset
@@ -1215,6 +1325,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   };
   while (step(std::integral_constant<uint32_t, 0>{}) && step(std::integral_constant<uint32_t, 1>{})) {
   }
+  span_end(span);
 }
 
 // 5c. BLAKE2b-256, one lane per segment.  No cross-lane traffic at all: the 16-word state,
@@ -1482,15 +1593,18 @@ hipError_t prepare_kernels() {
 
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
-                       uint32_t* unit_ctr, hipStream_t st) {
+                       uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
+                       uint64_t* n_entries, uint64_t* span, hipStream_t st) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   if (average_bits <= 32)
     cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
-                                                          mask64, ntiles, recs, unit_ctr);
+                                                          mask64, ntiles, recs, unit_ctr, done_ctr,
+                                                          entries, n_entries, span);
   else
     cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
-                                                         mask64, ntiles, recs, unit_ctr);
+                                                         mask64, ntiles, recs, unit_ctr, done_ctr,
+                                                         entries, n_entries, span);
   return hipGetLastError();
 }
 
@@ -1504,13 +1618,17 @@ hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uin
                          const uint64_t* n_entries, const uint64_t* offs,
                          const uint64_t* seg_base, uint32_t nfiles, uint32_t average_bits,
                          uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
-                         uint64_t* nseg, hipStream_t st) {
+                         uint64_t* nseg, uint32_t* done_ctr, pfscdc_segment* segs,
+                         uint64_t* seg_begin, uint32_t* order, uint32_t* counter,
+                         hipStream_t st) {
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   const uint64_t waves_per_block = kSelectBlock / 64;
   const uint64_t grid = (nfiles + waves_per_block - 1) / waves_per_block;
   select_kernel<<<(unsigned)grid, kSelectBlock, 0, st>>>(data, d_table, entries, n_entries,
                                                          offs, seg_base, nfiles, mask64,
-                                                         min_chunk, max_chunk, slots, nseg);
+                                                         min_chunk, max_chunk, slots, nseg,
+                                                         done_ctr, segs, seg_begin, order,
+                                                         counter);
   return hipGetLastError();
 }
 
@@ -1544,9 +1662,10 @@ static uint32_t hash_prio_blocks() {
 
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
-                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st) {
+                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
+                          bool ordered, uint64_t* span) {
   if (max_segments == 0) return hipSuccess;
-  hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
+  if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   static const int waves_per_simd = [] {  // tuning knob (PFSCDC_HASH_WAVES), default 2
     const char* e = getenv("PFSCDC_HASH_WAVES");
     const int w = e ? atoi(e) : kHashWavesPerSimd;
@@ -1565,7 +1684,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
   blake2b_kernel<kModeHash><<<(unsigned)grid, kHashBlock, 0, st>>>(
-      data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr, hash_prio_blocks());
+      data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr, hash_prio_blocks(),
+      span);
   return hipGetLastError();
 }
 
@@ -1586,7 +1706,8 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
   blake2b_kernel<kModeRefId><<<(unsigned)grid, kHashBlock, 0, st>>>(
-      data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out, hash_prio_blocks());
+      data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out, hash_prio_blocks(),
+      nullptr);
   return hipGetLastError();
 }
 
@@ -1600,7 +1721,8 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
   const uint64_t grid = need < full ? need : full;
   blake2b_kernel<kModeGet><<<(unsigned)grid, kHashBlock, 0, st>>>(
-      ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks());
+      ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
+      nullptr);
   return hipGetLastError();
 }
 

@@ -81,6 +81,9 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
   DevBuf<pfscdc_ref> d_refs;
   DevBuf<uint8_t> d_out;  // get_chunks: plaintext when the caller's output is on the host
+  DevBuf<uint64_t> d_span;  // kernel execution spans: scan begin/end, hash begin/end
+  PinnedBuf<uint64_t> h_span;
+  double wall_khz = 100000.0;  // s_memrealtime ticks per ms
   DevBuf<uint32_t> d_ids;  // fill_synthetic_pieces
   DevBuf<uint64_t> d_starts;
   PinnedBuf<pfscdc_ref> h_refs;
@@ -145,6 +148,14 @@ int validate_params(const pfscdc_params* p, std::string* why) {
   return PFSCDC_OK;
 }
 
+// Kernel spans start as (begin = ~0, end = 0): the kernels lower begin and raise end.
+hipError_t reset_spans(pfscdc_ctx* c, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(c->d_span.p, 0, 4 * sizeof(uint64_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_span.p, 0xFF, sizeof(uint64_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_span.p + 2, 0xFF, sizeof(uint64_t), st);
+  return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -193,6 +204,9 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    c->wall_khz = khz;
   if (hipError_t e = prepare_kernels(); e != hipSuccess) {
     std::fprintf(stderr, "pfscdc_ctx_create: kernel attributes: %s\n", hipGetErrorString(e));
     delete c;
@@ -242,6 +256,8 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->h_refs.release();
   c->d_out.release();
   c->d_ids.release();
+  c->d_span.release();
+  c->h_span.release();
   c->d_starts.release();
   c->h_offs.release();
   c->h_seg_base.release();
@@ -325,10 +341,12 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_qctr.ensure(2));
   if (options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
-  HIP_OK(c, c->d_unit_ctr.ensure(1));
+  HIP_OK(c, c->d_unit_ctr.ensure(3));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
+  HIP_OK(c, c->d_span.ensure(4));
+  HIP_OK(c, c->h_span.ensure(4));
 
   const uint8_t* data;
   if (bytes_on_device) {
@@ -352,29 +370,29 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
   // the scan adds candidates to the tile records with atomics
   if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
-  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, sizeof(uint32_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));  // + done counters
+  HIP_OK(c, reset_spans(c, st));
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
-  if (c->ntiles) {
+  if (c->ntiles) {  // scan + (last workgroup) compaction into the sorted entry list
     const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
-                          c->d_recs.p, grid, c->d_unit_ctr.p, st));
+                          c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1,
+                          c->d_entries.p, c->d_counts.p, c->d_span.p, st));
   }
   HIP_OK(c, hipEventRecord(c->ev[1], st));
-  if (c->ntiles)
-    HIP_OK(c, launch_compact(c->d_recs.p, c->ntiles, nbytes, c->d_entries.p, c->d_counts.p, st));
   HIP_OK(c, hipEventRecord(c->ev[2], st));
-  if (nfiles) {
+  if (nfiles)  // selection + (last workgroup) segment compaction and LPT order
     HIP_OK(c, launch_select(data, c->d_table, c->d_entries.p, c->d_counts.p, c->d_offs.p,
                             c->d_seg_base.p, nfiles, p.average_bits, (uint64_t)p.min_chunk,
-                            (uint64_t)p.max_chunk, c->d_slots.p, c->d_nseg.p, st));
-    HIP_OK(c, launch_segcompact(c->d_slots.p, c->d_seg_base.p, c->d_nseg.p, nfiles,
-                                c->d_segs.p, c->d_seg_begin.p, st));
-  }
+                            (uint64_t)p.max_chunk, c->d_slots.p, c->d_nseg.p,
+                            c->d_unit_ctr.p + 2, c->d_segs.p, c->d_seg_begin.p, c->d_order.p,
+                            c->d_qctr.p, st));
   HIP_OK(c, hipEventRecord(c->ev[3], st));
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
-                             c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st));
+                             c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
+                             c->d_span.p + 2));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
@@ -420,10 +438,27 @@ int pfscdc_wait(pfscdc_ctx* c) {
       HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, total * sizeof(pfscdc_ref),
                                hipMemcpyDeviceToHost, c->stream));
   }
+  HIP_OK(c, hipMemcpyAsync(c->h_span.p, c->d_span.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           c->stream));
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->nsegs = total;
   c->scan_valid = true;
+  return PFSCDC_OK;
+}
+
+int pfscdc_last_kernel_spans(pfscdc_ctx* c, float out[2]) {
+  if (!c || !out) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "scan pending");
+  if (!c->h_span.p) {  // no scan yet (spans are recorded by pfscdc_scan only)
+    out[0] = out[1] = 0.f;
+    return PFSCDC_OK;
+  }
+  const double ticks_per_ms = c->wall_khz;  // kHz = ticks per ms
+  for (int k = 0; k < 2; k++) {
+    const uint64_t a = c->h_span.p[2 * k], b = c->h_span.p[2 * k + 1];
+    out[k] = (b > a && a != ~0ULL) ? (float)((double)(b - a) / ticks_per_ms) : 0.f;
+  }
   return PFSCDC_OK;
 }
 
@@ -649,10 +684,11 @@ int pfscdc_candidates(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
   HIP_OK(c, c->d_recs.ensure(ntiles));
-  HIP_OK(c, c->d_unit_ctr.ensure(1));
+  HIP_OK(c, c->d_unit_ctr.ensure(3));
   HIP_OK(c, c->d_entries.ensure(ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
+  HIP_OK(c, c->d_span.ensure(4));
   const uint8_t* data;
   if (bytes_on_device) {
     data = (const uint8_t*)bytes;
@@ -667,13 +703,14 @@ int pfscdc_candidates(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
     HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main, hipMemcpyDeviceToDevice, st));
   HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
   HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * ntiles, st));
-  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, sizeof(uint32_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));
+  HIP_OK(c, reset_spans(c, st));
   HIP_OK(c, hipEventRecord(c->ev[0], st));
   const int grid = (int)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus);
   HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, c->params.average_bits, ntiles,
-                        c->d_recs.p, grid, c->d_unit_ctr.p, st));
+                        c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1, c->d_entries.p,
+                        c->d_counts.p, c->d_span.p, st));
   HIP_OK(c, hipEventRecord(c->ev[1], st));
-  HIP_OK(c, launch_compact(c->d_recs.p, ntiles, nbytes, c->d_entries.p, c->d_counts.p, st));
   HIP_OK(c, hipEventRecord(c->ev[2], st));
   uint64_t ne = 0;
   HIP_OK(c, hipMemcpyAsync(&ne, c->d_counts.p, sizeof ne, hipMemcpyDeviceToHost, st));

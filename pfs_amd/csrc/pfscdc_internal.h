@@ -82,20 +82,24 @@ uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
-                       uint32_t* unit_ctr, hipStream_t st);
+                       uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
+                       uint64_t* n_entries, uint64_t* span, hipStream_t st);
 hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
                           uint64_t* n_entries, hipStream_t st);
 hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,
                          const uint64_t* n_entries, const uint64_t* offs,
                          const uint64_t* seg_base, uint32_t nfiles, uint32_t average_bits,
                          uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
-                         uint64_t* nseg, hipStream_t st);
+                         uint64_t* nseg, uint32_t* done_ctr, pfscdc_segment* segs,
+                         uint64_t* seg_begin, uint32_t* order, uint32_t* counter,
+                         hipStream_t st);
 hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_base,
                              const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
                              uint64_t* seg_begin, hipStream_t st);
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
-                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st);
+                          uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
+                          bool ordered = false, uint64_t* span = nullptr);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
                         uint32_t* counter, hipStream_t st);
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,

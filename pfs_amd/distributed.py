@@ -330,8 +330,10 @@ def stream_segments(local, n: int, rng: tuple[int, int], halo: int, min_chunk: i
     # every rank knows every rank's range and every segment: plan the border copies
     ranges = gather_records(np.asarray([a, b], dtype=np.int64), device, group).reshape(-1, 2)
     ends = offs + sizes
+    # gloo (CPU tests, one-GPU rehearsals) moves host tensors only: stage device bytes
+    staged = local.is_cuda and dist.get_backend(group) == "gloo"
     ops = []
-    recv_views = []
+    recv_views = []  # (device view, host staging buffer)
     for q in range(world):
         qa, qb = int(ranges[q][0]), int(ranges[q][1])
         own = np.nonzero((offs >= qa) & (offs < qb))[0]
@@ -345,14 +347,19 @@ def stream_segments(local, n: int, rng: tuple[int, int], halo: int, min_chunk: i
                 continue
             if rank == p:  # send my bytes [lo, hi) to q
                 src = local[halo + (lo - a):halo + (hi - a)]
-                ops.append(dist.P2POp(dist.isend, src.contiguous(), q, group))
+                src = src.cpu() if staged else src.contiguous()
+                ops.append(dist.P2POp(dist.isend, src, q, group))
             elif rank == q:  # receive into the room after my range
                 dst = local[halo + (lo - a):halo + (hi - a)]
-                recv_views.append(dst)
-                ops.append(dist.P2POp(dist.irecv, dst, p, group))
+                buf = torch.empty(dst.numel(), dtype=torch.uint8) if staged else dst
+                recv_views.append((dst, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, p, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+        for dst, buf in recv_views:
+            if buf is not dst:
+                dst.copy_(buf)
     mine = np.nonzero((offs >= a) & (offs < b))[0]
     dt = _lib.segment_dtype()
     recs = np.zeros(len(mine), dtype=dt)
@@ -363,5 +370,4 @@ def stream_segments(local, n: int, rng: tuple[int, int], halo: int, min_chunk: i
         recs["size"] = sizes[mine]
         recs["flags"] = flags[mine]
         recs["hash"] = digests
-    del rank, torch
     return gather_records(recs, device, group)

@@ -68,17 +68,34 @@ def test_oracle_hit_rate_whole_file_dedup():
 
 
 def test_c4_layout_and_shards():
-    args = type("A", (), {"config": "c4", "seed": -1, "dedup": "blocks"})()
+    # c4 = the commit as pachd serializes it: whole filesets per rank, pieces tile every file
+    args = type("A", (), {"config": "c4", "seed": -1, "dedup": "blocks", "group": 1,
+                          "mem_threshold": 10 ** 9})()
     total = 0
     ranges = []
     for rank in range(8):
-        sizes, fbase, seed, mode, info, scaling = bench.workload(args, 8, rank)
-        assert scaling == "strong" and mode == SYNTH_RANDOM and seed == 0xC4
-        ranges.append((fbase, fbase + len(sizes)))
-        total += sum(sizes)
+        w = bench.workload(args, 8, rank)
+        assert w.scaling == "strong" and w.mode == SYNTH_RANDOM and w.seed == 0xC4
+        ranges.append((w.gbase, w.gbase + len(w.sizes)))
+        total += w.total
+        assert np.array_equal(w.gid, np.arange(*ranges[-1]))
     assert total == 100 * (1 << 30)
-    assert ranges[0][0] == 0 and ranges[-1][1] == bench.C4_FILES
+    lay = w.layout
+    assert ranges[0][0] == 0 and ranges[-1][1] == lay.npieces
     assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    assert lay.nfilesets == 108  # 100 GiB / 1e9 B
+
+
+def test_auto_group_holds_16k_chains():
+    args = type("A", (), {"config": "c4", "seed": -1, "dedup": "blocks", "group": 0,
+                          "mem_threshold": 10 ** 9})()
+    assert bench.workload(args, 1, 0).group == 1  # ~20K chains in one commit
+    w8 = bench.workload(args, 8, 3)
+    assert w8.group >= 6 and w8.total <= 180 << 30
+    # copy g holds the same pieces over files g * 10000 + f
+    n = w8.per_copy
+    assert np.array_equal(w8.ids[n:2 * n], w8.ids[:n] + bench.C4_FILES)
+    assert np.array_equal(w8.gid[n:2 * n], w8.gid[:n] + w8.layout.npieces)
 
 
 # ---------------------------------------------------------------- GPU
@@ -99,15 +116,21 @@ def test_device_generator_modes_match_host(mode):
 
 @gpu
 def test_shard_fill_keeps_global_file_ids():
+    # a rank's pieces of a commit cut into filesets hold exactly the commit's bytes there
     import torch
     sizes = [bench.C4_FILE_BYTES // 8] * 12
     offs = offsets(sizes)
     c = Chunker(ChunkParams(), 0)
     whole = synthetic_bytes(offs, 0xC4, SYNTH_DEDUP_BLOCKS)
-    for b, e in pd.shard_files(sizes, 3):
-        t = torch.empty(int(offs[e] - offs[b]), dtype=torch.uint8, device="cuda:0")
-        bench.fill(c, t, sizes[b:e], b, 0xC4, SYNTH_DEDUP_BLOCKS, np)
-        assert np.array_equal(t.cpu().numpy(), whole[int(offs[b]):int(offs[e])])
+    lay = pd.commit_layout(sizes, 3_000_000)
+    po = lay.offsets()
+    for rng in pd.shard_filesets(lay, 3):
+        p0, p1 = pd.rank_pieces(lay, rng)
+        w = bench.Work(lay.size[p0:p1], lay.file[p0:p1], lay.start[p0:p1], 0xC4,
+                       SYNTH_DEDUP_BLOCKS, {}, "strong", gbase=p0)
+        t = torch.empty(max(w.total, 1), dtype=torch.uint8, device="cuda:0")
+        bench.fill(c, t, w)
+        assert np.array_equal(t[:w.total].cpu().numpy(), whole[int(po[p0]):int(po[p1])])
 
 
 @gpu
