@@ -81,3 +81,52 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace("\"oracle\"", ""), f
+
+
+def _header_arities():
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for name, params in re.findall(r"\b(pfscdc_[a-z0-9_]+)\s*\(([^()]*)\)\s*;", text):
+        p = params.strip()
+        out[name] = 0 if p in ("", "void") else p.count(",") + 1
+    return out
+
+
+def _calls(code):
+    """(name, argument count) of every pfscdc_* call in code (top-level commas)."""
+    for m in re.finditer(r"\b(?:C\.)?(pfscdc_[a-z0-9_]+)\(", code):
+        depth, i, args, nonblank = 1, m.end(), 0, False
+        while depth:
+            ch = code[i]
+            if ch in "([{":
+                depth += 1
+            elif ch in ")]}":
+                depth -= 1
+            elif ch == "," and depth == 1:
+                args += 1
+            if depth and not ch.isspace():
+                nonblank = True
+            i += 1
+        yield m.group(1), (args + 1 if nonblank else 0)
+
+
+def test_cgo_stub_matches_header():
+    """The cgo binding in INTEGRATION.md (the reference-side stub a maintainer would add)
+    calls only functions pfscdc.h declares, each with its prototype's argument count, and
+    never hands C a Go pointer to keep (the cgo.Handle travels as an integer)."""
+    ar = _header_arities()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```go\n(.*?)```", doc, flags=re.S)
+    assert blocks
+    seen = set()
+    for code in blocks:
+        code = re.sub(r"//[^\n]*", "", code)  # comments
+        for name, n in _calls(code):
+            assert name in ar, name
+            assert n == ar[name], (name, n, ar[name])
+            seen.add(name)
+        assert "unsafe.Pointer(&g.handle)" not in code
+    for required in ("pfscdc_ctx_create", "pfscdc_writer_create", "pfscdc_writer_annotate",
+                     "pfscdc_writer_write", "pfscdc_writer_close", "pfscdc_set_options",
+                     "pfscdc_writer_set_store", "pfscdc_store_get", "pfscdc_writer_copy"):
+        assert required in seen, required

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-2 artifacts: GPU tests, smoke, PMC pass (FETCH_SIZE + SQ_INSTS_VALU per launch ->
+# traffic json), the default bench line, and a kernel-trace --stats pass of the bench's
+# 128 GiB steps (no e2e / literal / CPU legs, so every blake2b/scan launch is a 128 GiB one).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out && export TMPDIR=/tmp
+B="--no-cpu-baseline --no-e2e --no-literal"
+timeout -k 10 120 ./tools/valu_issue > gpurun_out/valu_issue.txt 2>&1 && \
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 && \
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 240 rocprofv3 --kernel-include-regex "blake2b|cdc_scan" --pmc FETCH_SIZE SQ_INSTS_VALU -d gpurun_out/pmc_fetch -o p --output-format csv -- python bench.py --steps 2 --warmup 1 $B > gpurun_out/pmc_fetch.log 2>&1 && \
+python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/traffic.json > gpurun_out/traffic.log 2>&1 && \
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 --traffic-json gpurun_out/traffic.json > gpurun_out/bench.json 2> gpurun_out/bench.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- python bench.py --steps 20 --warmup 5 $B > gpurun_out/prof_stats.log 2>&1
+rc=$?
+echo rc=$rc
+exit $rc
