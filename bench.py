@@ -91,7 +91,12 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
                          "one context + host thread each over the step's one input buffer); "
-                         "0 = auto: 2 for --path put on c2/c3 (1 if HBM cannot hold 2 inputs), else 1")
+                         "0 = auto: 2 for --path put on c3 (1 if HBM cannot hold 2 inputs), else 1")
+    ap.add_argument("--hash-order", default="free", choices=["serial", "free"],
+                    help="steps in flight: serial = a step's hash kernel starts after the "
+                         "previous step's (scans overlap hash tails; each hash launch has the "
+                         "GPU to itself, so its duration is its own); free = hashes of "
+                         "different steps may share the CUs")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the host threads the box allots (OMP_NUM_THREADS), else the "
                          "affinity mask")
@@ -99,8 +104,13 @@ def parse():
                     help="c2: configs[1] batches in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="c2: skip the two-in-flight throughput leg")
     ap.add_argument("--no-literal", action="store_true",
                     help="c2: skip the one-batch (unaggregated configs[1]) measurement")
+    ap.add_argument("--shard", default="",
+                    help="R/N: run rank R's share of an N-GPU job alone on this GPU (no "
+                         "collectives): the per-GPU rate an N-GPU run can reach")
     ap.add_argument("--traffic-json", default="",
                     help="per-launch HBM bytes / VALU counts from a PMC run (default: the "
                          "committed profiles/r2 pass of this workload, if any)")
@@ -304,14 +314,21 @@ def main():
     if args.config == "c3" and world > 1 and args.path == "put":
         return bench_c3_split(args, ctx)
 
-    work = workload(args, world, rank)
+    if args.shard:
+        sr, sn = (int(x) for x in args.shard.split("/"))
+        work = workload(args, sn, sr)
+        work.info["shard"] = "rank %d of %d, alone on one GPU" % (sr, sn)
+    else:
+        work = workload(args, world, rank)
     total = work.total
 
-    # Two steps in flight (two contexts on two streams, one resident input each): the next
-    # step's scan starts while this step's hash drains its longest chains (c2 +6%, c3 2x).
+    # One step at a time by default, so every kernel launch has the GPU to itself and its
+    # duration (HIP events, in-kernel span and a kernel trace alike) is its own.  c3 (one
+    # stream, bound by its longest 20 MB chains) runs two steps in flight on two contexts;
+    # c2's two-in-flight throughput is measured after the timed region (``two_in_flight``).
     # c4/c5 hold >= 16K chains per step through --group instead.
     S = args.inflight if args.inflight > 0 else (
-        2 if args.path == "put" and args.config in ("c2", "c3") else 1)
+        2 if args.path == "put" and args.config == "c3" else 1)
     batches = []
     for k in range(S):
         try:
@@ -329,6 +346,9 @@ def main():
             torch.cuda.empty_cache()
     S = len(batches)
     chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
+    if S > 1 and args.hash_order == "serial":  # each hash after the previous step's hash
+        for k in range(S):
+            chunkers[k].order_hash_after(chunkers[(k - 1) % S])
     for k, t in enumerate(batches):
         fill(chunkers[k], t, work)  # every step: the same workload
     if args.path == "get":
@@ -414,16 +434,18 @@ def main():
             r["traffic_source"] = tj["_source"] + " (FETCH_SIZE x 2, per launch)"
         return r
 
-    # the dominant kernel's duration = its execution span inside the kernel (first wavefront
-    # start to last wavefront end), averaged over the timed launches, as a kernel trace reports
-    hash_ms = kmean.get("hash_span") or kmean.get("hash")
-    scan_ms = kmean.get("scan_span") or kmean.get("scan")
+    # the dominant kernel's duration: HIP events around its launch on the library's stream,
+    # mean over the timed launches (= a kernel trace's per-launch duration when one step is
+    # in flight); the in-kernel span (first wavefront start to last wavefront end) beside it
+    hash_ms = kmean.get("hash")
+    scan_ms = kmean.get("scan")
     dom_hash = (hash_ms or 0) >= (scan_ms or 0)
     roofline = roof(hash_ms, "blake2b_kernel", "blake2b_kernel") if dom_hash else \
         roof(scan_ms, "cdc_scan_kernel", "cdc_scan_kernel")
-    roofline["duration_source"] = ("in-kernel s_memrealtime span (first wave start to last wave "
-                                   "end), mean over the %d timed launches" % len(steps_t))
-    roofline["event_ms"] = kmean.get("hash" if dom_hash else "scan")
+    roofline["duration_source"] = ("HIP events around the launch on the library's stream, mean "
+                                   "over the %d timed launches, %d step(s) in flight"
+                                   % (len(steps_t), S))
+    roofline["span_ms"] = kmean.get("hash_span" if dom_hash else "scan_span")
     if args.ref_ids and kmean.get("ref_ids", 0) > (hash_ms or 0):
         roofline = roof(kmean["ref_ids"], "blake2b_kernel<kModeRefId> (ChaCha20 + BLAKE2b of "
                                           "the ciphertext; HIP events)")
@@ -461,9 +483,10 @@ def main():
         "kernel_ms": kmean,
         "kernel_ms_median": kmed,
         "note": "kernel_ms: per step on this rank; scan/select/hash = HIP events on the "
-                "library's stream (they include waiting for CUs behind the other step in "
-                "flight), scan_span/hash_span = the kernels' own execution spans; the hash "
-                "is VALU-issue bound, not HBM bound (DESIGN.md §4)",
+                "library's stream (with steps in flight they include waiting for CUs behind "
+                "the other step), scan_span/hash_span = the kernels' own execution spans "
+                "(first wavefront start to last wavefront end); the hash is VALU-issue bound, "
+                "not HBM bound (DESIGN.md §4)",
         "cdc_only_gib_s": round(total / (scan_ms * 1e-3) / GIB, 2) if scan_ms else None,
         "roofline": roofline,
         "roofline_cdc": roofline_cdc,
@@ -499,11 +522,17 @@ def main():
 
     # the timed steps are done: release the other steps' inputs and contexts (the e2e
     # contexts below allocate their own device copies)
+    for k in range(len(chunkers)):
+        if S > 1:
+            chunkers[k].order_hash_after(None)
     for k in range(1, len(chunkers)):
         chunkers[k].close()
     del batches[1:]
     torch.cuda.empty_cache()
 
+    if rank == 0 and world == 1 and args.config == "c2" and S == 1 and not args.no_pipelined:
+        out["two_in_flight"] = two_in_flight(args, work, chunker, data, params, local, Chunker,
+                                             torch)
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_literal:
         out["configs1_literal"] = literal_batch(args, work, chunker, data, params, local,
                                                 Chunker, torch)
@@ -517,6 +546,47 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     chunker.close()
+
+
+def two_in_flight(args, work, chunker, data, params, local, Chunker, torch):
+    """After the timed region: the same steps with two in flight (a second context on its own
+    stream over its own copy of the input), so the next step's scan fills the CUs this step's
+    hash frees as its queue drains.  Reported beside the contract's one-at-a-time value."""
+    try:
+        data2 = torch.empty_like(data)
+    except torch.OutOfMemoryError:
+        return {"skipped": "HBM cannot hold a second input"}
+    data2.copy_(data)
+    other = Chunker(params, device=local)
+    pair, bufs, busy = [chunker, other], [data, data2], [False, False]
+    n, warm = 10, 2
+    t0 = None
+    for i in range(warm + n):
+        if i == warm:
+            for k in range(2):
+                if busy[k]:
+                    pair[k].wait()
+                    busy[k] = False
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        k = i % 2
+        if busy[k]:
+            pair[k].wait()
+        pair[k].scan_async(bufs[k], work.offs)
+        busy[k] = True
+    for j in range(2):
+        k = (warm + n + j) % 2
+        if busy[k]:
+            pair[k].wait()
+    el = time.perf_counter() - t0
+    other.close()
+    del data2
+    torch.cuda.empty_cache()
+    return {"value": round(work.total * n / el / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(el * 1e3 / n, 3), "steps": n,
+            "note": "two steps in flight on two contexts (hash kernels free to share CUs); "
+                    "per-kernel durations are then not a kernel's own, so the contract line "
+                    "runs one step at a time"}
 
 
 def literal_batch(args, work, chunker, data, params, local, Chunker, torch):

@@ -92,6 +92,13 @@ int pfscdc_set_stream(pfscdc_ctx* ctx, void* hip_stream);
  * stream before each call on a torch tensor. */
 int pfscdc_stream_wait(pfscdc_ctx* ctx, void* hip_stream);
 
+/* Steps in flight on two ctxs of one GPU: every later scan of ctx starts its BLAKE2b kernel
+ * only after the BLAKE2b kernel last enqueued by other (NULL: no ordering).  The next step's
+ * candidate scan still fills the CUs the current hash frees as its queue drains, but two
+ * hashes never share the SIMDs, so each hash launch runs for its own duration.  other must
+ * outlive the ordering (set NULL before destroying it). */
+int pfscdc_order_hash_after(pfscdc_ctx* ctx, pfscdc_ctx* other);
+
 /* CDC + content hash of a batch of files (one annotation each, concatenated).
  * Replaces, for every file of the batch, Writer.Annotate + Writer.Write + the hash part of
  * processChunk (writer.go:118-143,163-196,233-253,288-312): per-file cut positions and

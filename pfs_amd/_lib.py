@@ -45,7 +45,7 @@ EXPORTED = [
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
     "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
-    "pfscdc_last_kernel_spans",
+    "pfscdc_last_kernel_spans", "pfscdc_order_hash_after",
 ]
 
 
@@ -167,6 +167,7 @@ def load() -> C.CDLL:
             "pfscdc_last_error": (C.c_char_p, [vp]),
             "pfscdc_set_stream": (i32, [vp, vp]),
             "pfscdc_stream_wait": (i32, [vp, vp]),
+            "pfscdc_order_hash_after": (i32, [vp, vp]),
             "pfscdc_scan": (i32, [vp, vp, u64, i32, P(u64), u32]),
             "pfscdc_scan_async": (i32, [vp, vp, u64, i32, P(u64), u32]),
             "pfscdc_wait": (i32, [vp]),

@@ -92,6 +92,12 @@ class Chunker:
     def set_stream(self, stream_handle: Optional[int]) -> None:
         self._check(self.lib.pfscdc_set_stream(self.ctx, stream_handle or None), "set_stream")
 
+    def order_hash_after(self, other: Optional["Chunker"]) -> None:
+        """Start each later scan's BLAKE2b kernel after ``other``'s last enqueued one
+        (pfscdc_order_hash_after): steps in flight overlap scans with hash tails only."""
+        self._check(self.lib.pfscdc_order_hash_after(self.ctx, other.ctx if other else None),
+                    "order_hash_after")
+
     def _after_torch(self, *tensors) -> None:
         """Order the ctx stream after torch's current stream (pfscdc_stream_wait) when a
         call reads or writes torch CUDA tensors, so bytes written by a torch kernel or a

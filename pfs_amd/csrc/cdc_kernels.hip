@@ -1027,6 +1027,30 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
   "v_xor_b32 v111, v103, v105\n"                                       \
   "v_alignbit_b32 v102, v110, v111, 31\n"                              \
   "v_alignbit_b32 v103, v111, v110, 31\n"
+// The first G of a block: b, c, d are already in the column layout, so no DPP operands (an
+// identity quad_perm still costs the DPP issue rate): a + b and c + d are one v_lshl_add_u64
+// each, and the XORs are the 2-cycle VOP2 form (20 VALU instead of 22).
+#define PFS_G_ASM_PLAIN(X, Y)                                          \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, " X "\n"                  \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"             \
+  "v_xor_b32 v108, v107, v101\n"                                       \
+  "v_xor_b32 v109, v106, v100\n"                                       \
+  "v_lshl_add_u64 v[104:105], v[104:105], 0, v[108:109]\n"             \
+  "v_xor_b32 v110, v102, v104\n"                                       \
+  "v_xor_b32 v111, v103, v105\n"                                       \
+  "v_alignbit_b32 v102, v111, v110, 24\n"                              \
+  "v_alignbit_b32 v103, v110, v111, 24\n"                              \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, " Y "\n"                  \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"             \
+  "v_xor_b32 v110, v108, v100\n"                                       \
+  "v_xor_b32 v111, v109, v101\n"                                       \
+  "v_alignbit_b32 v106, v111, v110, 16\n"                              \
+  "v_alignbit_b32 v107, v110, v111, 16\n"                              \
+  "v_lshl_add_u64 v[104:105], v[104:105], 0, v[106:107]\n"             \
+  "v_xor_b32 v110, v102, v104\n"                                       \
+  "v_xor_b32 v111, v103, v105\n"                                       \
+  "v_alignbit_b32 v102, v110, v111, 31\n"                              \
+  "v_alignbit_b32 v103, v111, v110, 31\n"
 #define PFS_QP_ID "[0,1,2,3]"
 #define PFS_QP_R1 "[1,2,3,0]"  // 0x39: lane j reads lane j+1
 #define PFS_QP_R2 "[2,3,0,1]"  // 0x4E
@@ -1039,7 +1063,8 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 #define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                            \
   do {                                                                                  \
     if (FIRST)                                                                          \
-      asm volatile(PFS_ROUND_ASM(PFS_QP_ID, PFS_QP_ID, PFS_QP_ID)                      \
+      asm volatile("s_nop 1\n" PFS_G_ASM_PLAIN("%[x0]", "%[x1]")                        \
+                   PFS_G_ASM(PFS_QP_R1, PFS_QP_R2, PFS_QP_R3, "%[x2]", "%[x3]")          \
                    : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c),        \
                      "+{v[106:107]}"(d)                                                 \
                    : [x0] "v"(x0_), [x1] "v"(x1_), [x2] "v"(x2_), [x3] "v"(x3_)          \

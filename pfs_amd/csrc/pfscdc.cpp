@@ -105,6 +105,7 @@ struct pfscdc_ctx {
   uint64_t slot_cap = 0;
   uint64_t nsegs = 0;
   const uint8_t* dev_data = nullptr;  // data pointer of the last scan
+  pfscdc_ctx* hash_after = nullptr;   // pfscdc_order_hash_after
 };
 
 namespace pfscdc {
@@ -281,6 +282,12 @@ int pfscdc_set_stream(pfscdc_ctx* c, void* hip_stream) {
   return PFSCDC_OK;
 }
 
+int pfscdc_order_hash_after(pfscdc_ctx* c, pfscdc_ctx* other) {
+  if (!c || other == c) return PFSCDC_EINVAL;
+  c->hash_after = other;
+  return PFSCDC_OK;
+}
+
 int pfscdc_stream_wait(pfscdc_ctx* c, void* hip_stream) {
   if (!c) return PFSCDC_EINVAL;
   hipStream_t s = (hipStream_t)hip_stream;
@@ -389,6 +396,10 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                             c->d_unit_ctr.p + 2, c->d_segs.p, c->d_seg_begin.p, c->d_order.p,
                             c->d_qctr.p, st));
   HIP_OK(c, hipEventRecord(c->ev[3], st));
+  // steps in flight on several ctxs: this step's hash starts after the other ctx's last
+  // enqueued hash (the scans still overlap the hash tails; two hashes never share the CUs)
+  if (c->hash_after && c->hash_after->device == c->device)
+    HIP_OK(c, hipStreamWaitEvent(st, c->hash_after->ev[4], 0));
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
