@@ -21,7 +21,7 @@ Workloads (--config, BASELINE.json configs[i]; all synthetic, generated in HBM):
      cut into serialized filesets of --mem-threshold bytes as pachd's UnorderedWriter does;
      ranks take whole filesets (a file cut at a fileset border is two pieces), so the
      gathered index equals N=1's.  --group G commits per step per rank (auto: enough for
-     >= 16K BLAKE2b chains per GPU).
+     >= 20K BLAKE2b chains per GPU).
   c5: configs[4], the c4 layout with dedup-heavy bytes: 1 MiB blocks, half of them copies of
      64 pooled blocks (--dedup blocks) or half of the files copies of 64 pooled files
      (--dedup files); reports the segment / byte dedup hit rate of the gathered index.
@@ -53,7 +53,9 @@ VALU_PEAK_GIPS = 1024 * 2.4 / 4.0
 GIB = float(1 << 30)
 C4_FILES, C4_FILE_BYTES, C4_TAIL = 10_000, 10_737_418, 2_400
 C3_BYTES = 10 * (1 << 30)
-MIN_CHAINS = 16384  # BLAKE2b chains per GPU per step for the hash to reach its issue bound
+# BLAKE2b chains per GPU per step for the hash to reach its issue bound (c4 rank 0 of 8 alone
+# on one GPU: 16K chains 545 GiB/s, 21K chains 696 GiB/s, N=1's 20.5K 661; profiles/r2/scale/)
+MIN_CHAINS = 20480
 
 
 def parse():
@@ -66,7 +68,7 @@ def parse():
     ap.add_argument("--file-bytes", type=int, default=4 << 20, help="c2: bytes per file")
     ap.add_argument("--group", type=int, default=0,
                     help="c2: configs[1] batches per step (default 32 = 128 GiB resident); "
-                         "c4/c5: commits per step per rank (default: enough for >= 16K "
+                         "c4/c5: commits per step per rank (default: enough for >= 20K "
                          "chains per GPU); c3: 1")
     ap.add_argument("--dedup", default="blocks", choices=["blocks", "files"], help="c5 layout")
     ap.add_argument("--ref-ids", action="store_true",

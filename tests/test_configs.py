@@ -86,12 +86,12 @@ def test_c4_layout_and_shards():
     assert lay.nfilesets == 108  # 100 GiB / 1e9 B
 
 
-def test_auto_group_holds_16k_chains():
+def test_auto_group_holds_20k_chains():
     args = type("A", (), {"config": "c4", "seed": -1, "dedup": "blocks", "group": 0,
                           "mem_threshold": 10 ** 9})()
     assert bench.workload(args, 1, 0).group == 1  # ~20K chains in one commit
     w8 = bench.workload(args, 8, 3)
-    assert w8.group >= 6 and w8.total <= 180 << 30
+    assert w8.group == 8 and w8.total <= 180 << 30
     # copy g holds the same pieces over files g * 10000 + f
     n = w8.per_copy
     assert np.array_equal(w8.ids[n:2 * n], w8.ids[:n] + bench.C4_FILES)
