@@ -805,11 +805,13 @@ PFS_DEV T pick4(uint32_t j, T v0, T v1, T v2, T v3) {
 }
 
 // Per (round, lane): byte offsets (word*8) of the 4 message words the lane consumes:
-// column G_j uses sigma[r][2j], sigma[r][2j+1]; diagonal G_{4+j} uses sigma[r][8+2j], [9+2j].
+// column G_j uses sigma[r][2j], sigma[r][2j+1]; the diagonal step runs G_{4+i}, i = (j+3)%4,
+// on sigma[r][8+2i], [9+2i] (see PFS_ROUND: row b never leaves its lane).
 constexpr uint32_t kSigmaPack[12][4] = {
 #define PK(a, b, c, d) ((uint32_t)(a) * 8u | (uint32_t)(b) * 8u << 8 | (uint32_t)(c) * 8u << 16 | (uint32_t)(d) * 8u << 24)
+// b stays in its lane; lane j computes the diagonal through b_j, G_{4+(j+3)%4}
 #define ROW(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
-  {PK(s0, s1, s8, s9), PK(s2, s3, s10, s11), PK(s4, s5, s12, s13), PK(s6, s7, s14, s15)}
+  {PK(s0, s1, s14, s15), PK(s2, s3, s8, s9), PK(s4, s5, s10, s11), PK(s6, s7, s12, s13)}
     ROW(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15),
     ROW(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3),
     ROW(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4),
@@ -996,24 +998,27 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 // in fixed registers a = v[100:101], b = v[102:103], c = v[104:105], d = v[106:107] (temps
 // v108-v111) so 64-bit ops (v_lshl_add_u64) and their 32-bit halves (DPP, alignbit) can be
 // named; the compiler-scheduled form spends ~26 VALU per G on register-pair copies and
-// separate DPP moves.  Here each G is 22 VALU: the incoming quad rotation of b, c and d is
-// a DPP source operand of their first uses (v_add_co_u32_dpp / v_addc_co_u32_dpp for
-// a + b' and c' + d, v_xor_b32_dpp for d' ^ a and b' ^ c), so nothing is moved.
-// Hazards: a DPP read needs 2 wait states after the VALU write of its source; inside a G
-// the closest pair is b (written by the last two instructions of the previous G, read by
-// instructions 2-3), covered by the a + x add in between; each round starts with s_nop 1
-// for whatever the compiler placed before it.
+// separate DPP moves.  Here each G is 22 VALU and nothing is moved between lanes on its own:
+// row b never leaves its lane (lane j runs the diagonal through b_j, G_{4+(j+3)%4}), and the
+// quad rotation of rows a, c and d, into the diagonal layout and back, is a DPP source
+// operand of their first uses: a' + x and c' + d (v_add_co_u32_dpp / v_addc_co_u32_dpp),
+// d' ^ a (v_xor_b32_dpp).  Keeping b in place rather than a (the textbook choice) leaves
+// b ^ c in the 2-cycle plain v_xor_b32 form: 16 four-cycle + 6 two-cycle ops per G instead
+// of 18 + 4 (issue-rate table).
+// Hazards: a DPP read needs 2 wait states after the VALU write of its source; the DPP sources
+// here (a, c, d) were last written 6+ instructions earlier, and each round starts with
+// s_nop 1 for whatever the compiler placed before it.
 #define PFS_DPP(P) " quad_perm:" P " row_mask:0xf bank_mask:0xf\n"
-#define PFS_G_ASM(PB, PC, PD, X, Y)                                    \
-  "v_lshl_add_u64 v[100:101], v[100:101], 0, " X "\n"                  \
-  "v_add_co_u32_dpp v100, vcc, v102, v100" PFS_DPP(PB)                 \
-  "v_addc_co_u32_dpp v101, vcc, v103, v101, vcc" PFS_DPP(PB)           \
+#define PFS_G_ASM(PA, PC, PD, XL, XH, Y)                               \
+  "v_add_co_u32_dpp v100, vcc, v100, " XL PFS_DPP(PA)                  \
+  "v_addc_co_u32_dpp v101, vcc, v101, " XH ", vcc" PFS_DPP(PA)         \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"             \
   "v_xor_b32_dpp v108, v107, v101" PFS_DPP(PD)                         \
   "v_xor_b32_dpp v109, v106, v100" PFS_DPP(PD)                         \
   "v_add_co_u32_dpp v104, vcc, v104, v108" PFS_DPP(PC)                 \
   "v_addc_co_u32_dpp v105, vcc, v105, v109, vcc" PFS_DPP(PC)           \
-  "v_xor_b32_dpp v110, v102, v104" PFS_DPP(PB)                         \
-  "v_xor_b32_dpp v111, v103, v105" PFS_DPP(PB)                         \
+  "v_xor_b32 v110, v102, v104\n"                                       \
+  "v_xor_b32 v111, v103, v105\n"                                       \
   "v_alignbit_b32 v102, v111, v110, 24\n"                              \
   "v_alignbit_b32 v103, v110, v111, 24\n"                              \
   "v_lshl_add_u64 v[100:101], v[100:101], 0, " Y "\n"                  \
@@ -1027,9 +1032,9 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
   "v_xor_b32 v111, v103, v105\n"                                       \
   "v_alignbit_b32 v102, v110, v111, 31\n"                              \
   "v_alignbit_b32 v103, v111, v110, 31\n"
-// The first G of a block: b, c, d are already in the column layout, so no DPP operands (an
-// identity quad_perm still costs the DPP issue rate): a + b and c + d are one v_lshl_add_u64
-// each, and the XORs are the 2-cycle VOP2 form (20 VALU instead of 22).
+// The first G of a block: a, c, d are already in the column layout, so no DPP operands (an
+// identity quad_perm still costs the DPP issue rate): a + x and c + d are one v_lshl_add_u64
+// each, and d ^ a is the 2-cycle VOP2 form (20 VALU instead of 22).
 #define PFS_G_ASM_PLAIN(X, Y)                                          \
   "v_lshl_add_u64 v[100:101], v[100:101], 0, " X "\n"                  \
   "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"             \
@@ -1054,27 +1059,25 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 #define PFS_QP_ID "[0,1,2,3]"
 #define PFS_QP_R1 "[1,2,3,0]"  // 0x39: lane j reads lane j+1
 #define PFS_QP_R2 "[2,3,0,1]"  // 0x4E
-#define PFS_QP_R3 "[3,0,1,2]"  // 0x93
-// column G (its b, c, d arrive in the previous diagonal layout: undo it on first use), then
-// diagonal G (b <- lane j+1, c <- j+2, d <- j+3)
-#define PFS_ROUND_ASM(PB0, PC0, PD0)                                          \
-  "s_nop 1\n" PFS_G_ASM(PB0, PC0, PD0, "%[x0]", "%[x1]")                      \
-      PFS_G_ASM(PFS_QP_R1, PFS_QP_R2, PFS_QP_R3, "%[x2]", "%[x3]")
-#define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                            \
-  do {                                                                                  \
-    if (FIRST)                                                                          \
-      asm volatile("s_nop 1\n" PFS_G_ASM_PLAIN("%[x0]", "%[x1]")                        \
-                   PFS_G_ASM(PFS_QP_R1, PFS_QP_R2, PFS_QP_R3, "%[x2]", "%[x3]")          \
-                   : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c),        \
-                     "+{v[106:107]}"(d)                                                 \
-                   : [x0] "v"(x0_), [x1] "v"(x1_), [x2] "v"(x2_), [x3] "v"(x3_)          \
-                   : "vcc", "v108", "v109", "v110", "v111");                            \
-    else                                                                                \
-      asm volatile(PFS_ROUND_ASM(PFS_QP_R3, PFS_QP_R2, PFS_QP_R1)                      \
-                   : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c),        \
-                     "+{v[106:107]}"(d)                                                 \
-                   : [x0] "v"(x0_), [x1] "v"(x1_), [x2] "v"(x2_), [x3] "v"(x3_)          \
-                   : "vcc", "v108", "v109", "v110", "v111");                            \
+#define PFS_QP_R3 "[3,0,1,2]"  // 0x93: lane j reads lane j-1
+// Diagonal step on lane j: a_{j-1}, b_j, c_{j+1}, d_{j+2} (R3, -, R1, R2); the next column
+// step takes a, c, d back from the diagonal layout (R1, -, R3, R2).
+#define PFS_DIAG_G PFS_G_ASM(PFS_QP_R3, PFS_QP_R1, PFS_QP_R2, "%[x2l]", "%[x2h]", "%[x3]")
+#define PFS_ROUND_OPS(x0_, x1_, x2_, x3_)                                                \
+  : "+{v[100:101]}"(a), "+{v[102:103]}"(b), "+{v[104:105]}"(c), "+{v[106:107]}"(d)      \
+  : [x0] "v"(x0_), [x0l] "v"((uint32_t)(x0_)), [x0h] "v"((uint32_t)((x0_) >> 32)),      \
+    [x1] "v"(x1_), [x2l] "v"((uint32_t)(x2_)), [x2h] "v"((uint32_t)((x2_) >> 32)),       \
+    [x3] "v"(x3_)                                                                        \
+  : "vcc", "v108", "v109", "v110", "v111"
+#define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                                  \
+  do {                                                                                        \
+    if (FIRST)                                                                                \
+      asm volatile("s_nop 1\n" PFS_G_ASM_PLAIN("%[x0]", "%[x1]") PFS_DIAG_G                    \
+                 PFS_ROUND_OPS(x0_, x1_, x2_, x3_));                                          \
+    else                                                                                      \
+      asm volatile("s_nop 1\n" PFS_G_ASM(PFS_QP_R1, PFS_QP_R3, PFS_QP_R2, "%[x0l]", "%[x0h]", \
+                                         "%[x1]") PFS_DIAG_G                                   \
+                 PFS_ROUND_OPS(x0_, x1_, x2_, x3_));                                          \
   } while (0)
 
 // MODE kModeHash:  DataRef.Hash = BLAKE2b-256(segment) into segs[].hash.
@@ -1297,15 +1300,15 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       }
 #ifdef PFS_HASH_CXX
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
-      c = quad_perm64<0x4E>(c);            // c <- v[8+(j+2)%4]
-      d = quad_perm64<0x93>(d);            // d <- v[12+(j+3)%4]
-      b = quad_perm64<0x39>(b);            // b <- v[4+(j+1)%4]
-      PFS_G(a, b, c, d, x2, x3);           // diagonal step: G_{4+j}
-      c = quad_perm64<0x4E>(c);
-      d = quad_perm64<0x39>(d);
-      b = quad_perm64<0x93>(b);
+      a = quad_perm64<0x93>(a);            // a <- v[(j+3)%4]
+      c = quad_perm64<0x39>(c);            // c <- v[8+(j+1)%4]
+      d = quad_perm64<0x4E>(d);            // d <- v[12+(j+2)%4]
+      PFS_G(a, b, c, d, x2, x3);           // diagonal step through b_j: G_{4+(j+3)%4}
+      a = quad_perm64<0x39>(a);
+      c = quad_perm64<0x93>(c);
+      d = quad_perm64<0x4E>(d);
 #else
-      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves b, c, d in the diagonal layout
+      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves a, c, d in the diagonal layout
 #endif
       x0 = y0; x1 = y1; x2 = y2; x3 = y3;
       if (r == 5 && active && !last) {  // block blk+1 -> the other buffer; fetch blk+2
@@ -1314,9 +1317,9 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       }
     }
 #ifndef PFS_HASH_CXX
-    c = quad_perm64<0x4E>(c);  // back to the column layout
-    d = quad_perm64<0x39>(d);
-    b = quad_perm64<0x93>(b);
+    a = quad_perm64<0x39>(a);  // back to the column layout
+    c = quad_perm64<0x93>(c);
+    d = quad_perm64<0x4E>(d);
 #endif
     ha ^= a ^ c;
     hb ^= b ^ d;
