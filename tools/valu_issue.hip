@@ -54,6 +54,9 @@
 #define PKFMA(R) "v_pk_fma_f32 " R ", " R ", %12, " R "\n"
 #define PKADDF(R) "v_pk_add_f32 " R ", " R ", %12\n"
 #define PKMOV(R) "v_pk_mov_b32 " R ", %12, " R " op_sel:[0,1]\n"
+#define XSDWA(R) "v_xor_b32_sdwa " R ", " R ", %12 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n"
+#define XSDWAP(R) "v_xor_b32_sdwa " R ", " R ", %12 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n"
+#define MIXXA(R) XOR(R) ALB(R)  /* one VOP2 + one VOP3 per chain step (counted as 2) */
 
 template <int K>
 __global__ __launch_bounds__(256) void thr(uint64_t* out, uint32_t seed) {
@@ -103,6 +106,9 @@ __global__ __launch_bounds__(256) void thr(uint64_t* out, uint32_t seed) {
       if constexpr (K == 17) CH12(ADDF);
       if constexpr (K == 18) CH12(FMAF);
       if constexpr (K == 19) CH12(PKADD16);
+      if constexpr (K == 20) CH12(XSDWA);
+      if constexpr (K == 21) CH12(XSDWAP);
+      if constexpr (K == 22) CH12(MIXXA);
     }
     t1 = __builtin_amdgcn_s_memtime();
     uint32_t s = 0;
@@ -128,7 +134,8 @@ int main() {
       {"v_mov_b32_dpp", thr<15>},   {"v_cndmask_b32", thr<16>},    {"v_add_f32", thr<17>},
       {"v_fma_f32", thr<18>},       {"v_pk_add_u16", thr<19>},     {"v_lshl_add_u64", thr<100>},
       {"v_lshlrev_b64", thr<101>},  {"v_pk_fma_f32", thr<102>},    {"v_pk_add_f32", thr<103>},
-      {"v_pk_mov_b32", thr<104>},
+      {"v_pk_mov_b32", thr<104>},   {"v_xor_b32_sdwa (word, preserve)", thr<20>},
+      {"v_xor_b32_sdwa (word, pad)", thr<21>}, {"v_xor_b32 + v_alignbit_b32 (per pair)", thr<22>},
   };
   int ncu = 256;
   hipDeviceProp_t prop;
