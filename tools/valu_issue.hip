@@ -57,6 +57,19 @@
 #define XSDWA(R) "v_xor_b32_sdwa " R ", " R ", %12 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n"
 #define XSDWAP(R) "v_xor_b32_sdwa " R ", " R ", %12 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n"
 #define MIXXA(R) XOR(R) ALB(R)  /* one VOP2 + one VOP3 per chain step (counted as 2) */
+// runs of k simple ops then k 4-cycle ops over k chains (each chain: one of each per step)
+#define RUNS(K, OPS_X, OPS_A) asm volatile(".rept 4\n" OPS_X OPS_A ".endr\n" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), \
+    "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]) : "v"(b), "v"(c))
+#define X2(a0, a1) XOR(a0) XOR(a1)
+#define A2(a0, a1) ALB(a0) ALB(a1)
+#define RUN2 RUNS(2, X2("%0", "%1") A2("%0", "%1") X2("%2", "%3") A2("%2", "%3") X2("%4", "%5") A2("%4", "%5") \
+    X2("%6", "%7") A2("%6", "%7") X2("%8", "%9") A2("%8", "%9") X2("%10", "%11") A2("%10", "%11"), "")
+#define RUN3 RUNS(3, X2("%0", "%1") XOR("%2") A2("%0", "%1") ALB("%2") X2("%3", "%4") XOR("%5") A2("%3", "%4") ALB("%5") \
+    X2("%6", "%7") XOR("%8") A2("%6", "%7") ALB("%8") X2("%9", "%10") XOR("%11") A2("%9", "%10") ALB("%11"), "")
+#define RUN6 RUNS(6, X2("%0", "%1") X2("%2", "%3") X2("%4", "%5") A2("%0", "%1") A2("%2", "%3") A2("%4", "%5") \
+    X2("%6", "%7") X2("%8", "%9") X2("%10", "%11") A2("%6", "%7") A2("%8", "%9") A2("%10", "%11"), "")
+#define RUN12 RUNS(12, X2("%0", "%1") X2("%2", "%3") X2("%4", "%5") X2("%6", "%7") X2("%8", "%9") X2("%10", "%11"), \
+    A2("%0", "%1") A2("%2", "%3") A2("%4", "%5") A2("%6", "%7") A2("%8", "%9") A2("%10", "%11"))
 
 template <int K>
 __global__ __launch_bounds__(256) void thr(uint64_t* out, uint32_t seed) {
@@ -109,6 +122,10 @@ __global__ __launch_bounds__(256) void thr(uint64_t* out, uint32_t seed) {
       if constexpr (K == 20) CH12(XSDWA);
       if constexpr (K == 21) CH12(XSDWAP);
       if constexpr (K == 22) CH12(MIXXA);
+      if constexpr (K == 23) RUN2;
+      if constexpr (K == 24) RUN3;
+      if constexpr (K == 25) RUN6;
+      if constexpr (K == 26) RUN12;
     }
     t1 = __builtin_amdgcn_s_memtime();
     uint32_t s = 0;
@@ -136,6 +153,8 @@ int main() {
       {"v_lshlrev_b64", thr<101>},  {"v_pk_fma_f32", thr<102>},    {"v_pk_add_f32", thr<103>},
       {"v_pk_mov_b32", thr<104>},   {"v_xor_b32_sdwa (word, preserve)", thr<20>},
       {"v_xor_b32_sdwa (word, pad)", thr<21>}, {"v_xor_b32 + v_alignbit_b32 (per pair)", thr<22>},
+      {"runs of 2 xor / 2 alignbit (per pair)", thr<23>}, {"runs of 3 / 3 (per pair)", thr<24>},
+      {"runs of 6 / 6 (per pair)", thr<25>},  {"runs of 12 / 12 (per pair)", thr<26>},
   };
   int ncu = 256;
   hipDeviceProp_t prop;
