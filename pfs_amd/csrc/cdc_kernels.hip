@@ -369,7 +369,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
         WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
   }
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t lane_off = (lane & 31u) * 8u;
   uint8_t* wbuf = smem + kTableLdsBytes + wave * kStageBytes;
   const uint32_t rd_base = lane * 128u;
@@ -405,6 +406,14 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     if (wave_base < n) {  // wave-uniform
       const bool fast = wave_base + 64 * (uint64_t)kStrip <= n_main;
       auto dma_step = [&](uint32_t step) {
+        if (fast) {  // wave-uniform: a scalar base plus the lane's 32-bit offset, LDS dst in M0
+          const uint8_t* base = data + (wave_base + step * 128u);
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(base + dma_off[i]),
+                (__attribute__((address_space(3))) void*)(wbuf + i * 1024), 16, 0, 0);
+          return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
           const uint64_t p = wave_base + dma_off[i] + step * 128u;
