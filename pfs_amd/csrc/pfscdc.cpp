@@ -86,6 +86,7 @@ struct pfscdc_ctx {
   double wall_khz = 100000.0;  // s_memrealtime ticks per ms
   DevBuf<uint32_t> d_ids;  // fill_synthetic_pieces
   DevBuf<uint64_t> d_starts;
+  DevBuf<uint8_t> d_group, d_group_ct;  // writers_close_group: staged bytes, ciphertexts
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
   float get_ms = 0.f;
@@ -260,6 +261,8 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_span.release();
   c->h_span.release();
   c->d_starts.release();
+  c->d_group.release();
+  c->d_group_ct.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -871,6 +874,14 @@ int pfscdc_fill_synthetic(pfscdc_ctx* c, void* dev_bytes, const uint64_t* file_o
 namespace pfscdc {
 
 int ctx_device(const pfscdc_ctx* c) { return c->device; }
+hipError_t ctx_group_buffers(pfscdc_ctx* c, uint64_t bytes, bool ctext, uint8_t** d,
+                             uint8_t** dct) {
+  hipError_t e = c->d_group.ensure(bytes);
+  if (e == hipSuccess && ctext) e = c->d_group_ct.ensure(bytes);
+  *d = e == hipSuccess ? c->d_group.p : nullptr;
+  *dct = e == hipSuccess && ctext ? c->d_group_ct.p : nullptr;
+  return e;
+}
 uint32_t ctx_options(const pfscdc_ctx* c) { return c->options; }
 bool ctx_scan_valid(const pfscdc_ctx* c) { return c->scan_valid && !c->pending; }
 uint32_t ctx_nfiles(const pfscdc_ctx* c) { return c->nfiles; }

@@ -69,6 +69,10 @@ int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
                        const uint64_t* offs, uint32_t n, uint8_t* hashes, const uint8_t* known,
                        pfscdc_ref* refs, uint8_t* ctext_out = nullptr);
 int ctx_device(const pfscdc_ctx* ctx);
+// grow-only device staging owned by the ctx (writers_close_group): bytes, and the
+// ciphertexts when ctext; both stay valid until the next call or pfscdc_ctx_destroy
+hipError_t ctx_group_buffers(pfscdc_ctx* ctx, uint64_t bytes, bool ctext, uint8_t** d,
+                             uint8_t** dct);
 // pfscdc_writer_close of n writers on one ctx with one scan and one chunk.Create pass
 int writers_close_group(pfscdc_writer* const* ws, size_t n);
 // a write whose bytes stay owned by the caller until the writer flushes or closes

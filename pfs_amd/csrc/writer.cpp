@@ -646,8 +646,10 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
   uint8_t *d = nullptr, *dct = nullptr;
   const bool up = ws[0]->upload && ws[0]->store;
   int rc = PFSCDC_OK;
-  if (hipSetDevice(ctx_device(ctx)) != hipSuccess || hipMalloc((void**)&d, total + 64) != hipSuccess ||
-      (up && hipMalloc((void**)&dct, total + 64) != hipSuccess))
+  // the ctx's grow-only staging: a commit closes many groups, and a fresh hipMalloc/hipFree
+  // of up to the group's size per close would dominate small groups
+  if (hipSetDevice(ctx_device(ctx)) != hipSuccess ||
+      ctx_group_buffers(ctx, total + 64, up, &d, &dct) != hipSuccess)
     rc = PFSCDC_ENOMEM;
   for (size_t i = 0; i < n && !rc; i++) {
     const pfscdc_writer* w = ws[i];
@@ -720,8 +722,6 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
     }
   }
   const auto t4 = now();
-  if (d) (void)hipFree(d);
-  if (dct) (void)hipFree(dct);
   for (size_t i = 0; i < n; i++) {
     pfscdc_writer* w = ws[i];
     w->closed = true;
