@@ -1365,6 +1365,87 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   span_end(span);
 }
 
+// 5d. ChaCha20 ciphertext of whole chunks, one lane per 64-byte keystream block (the Ref.Id
+// pass split in two for chunk lists that cannot fill the GPU, see create_refs_device).  Every
+// block is independent (RFC 8439 §2.4: counter = block index within the chunk, zero nonce,
+// key = the chunk's dek), so this pass runs at the VALU rate however long the chunks are,
+// and the serial BLAKE2b chain that follows no longer carries the keystream.  Record r
+// covers blocks [blk_base[r], blk_base[r+1]); consecutive lanes take consecutive blocks.
+PFS_DEV uint32_t rotl32v(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+#define PFS_CQR(a, b, c, d)                         \
+  do {                                              \
+    x[a] += x[b]; x[d] = rotl32v(x[d] ^ x[a], 16);  \
+    x[c] += x[d]; x[b] = rotl32v(x[b] ^ x[c], 12);  \
+    x[a] += x[b]; x[d] = rotl32v(x[d] ^ x[a], 8);   \
+    x[c] += x[d]; x[b] = rotl32v(x[b] ^ x[c], 7);   \
+  } while (0)
+__global__ __launch_bounds__(256) void chacha_xor_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
+    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out) {
+  const uint64_t nblocks = blk_base[n];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  // wave-uniform window of 64 consecutive blocks: the record of its first block by a scalar
+  // binary search, then each lane steps forward over the (rare) record ends in the window
+  const uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x +
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+  for (uint64_t g0 = w0; g0 < nblocks; g0 += stride) {
+    uint32_t lo = 0, hi = n;  // the last r with blk_base[r] <= g0
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (blk_base[mid] <= g0) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t g = g0 + lane;
+    if (g >= nblocks) continue;
+    while (blk_base[lo + 1] <= g) lo++;
+    const pfscdc_segment& sg = segs[lo];
+    const uint64_t b = g - blk_base[lo];
+    const uint64_t at = offs[sg.file] + sg.offset + 64 * b;
+    const int64_t avail = (int64_t)(sg.size - 64 * b);
+    const uint4 k0 = reinterpret_cast<const uint4*>(refs[lo].dek)[0];
+    const uint4 k1 = reinterpret_cast<const uint4*>(refs[lo].dek)[1];
+    const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                            k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w,
+                            (uint32_t)b, 0u, 0u, 0u};
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = s[i];
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+      PFS_CQR(0, 4, 8, 12);
+      PFS_CQR(1, 5, 9, 13);
+      PFS_CQR(2, 6, 10, 14);
+      PFS_CQR(3, 7, 11, 15);
+      PFS_CQR(0, 5, 10, 15);
+      PFS_CQR(1, 6, 11, 12);
+      PFS_CQR(2, 7, 8, 13);
+      PFS_CQR(3, 4, 9, 14);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] += s[i];
+    const uint8_t* src = data + at;
+    uint8_t* dst = out + at;
+    if (avail >= 64) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint4 v;
+        __builtin_memcpy(&v, src + 16 * q, 16);
+        v.x ^= x[4 * q];
+        v.y ^= x[4 * q + 1];
+        v.z ^= x[4 * q + 2];
+        v.w ^= x[4 * q + 3];
+        __builtin_memcpy(dst + 16 * q, &v, 16);
+      }
+    } else {  // the chunk's last block: only its own bytes (the next chunk's follow)
+      for (int64_t k = 0; k < avail; k++)
+        dst[k] = src[k] ^ (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+#undef PFS_CQR
+
 // 5c. BLAKE2b-256, one lane per segment.  No cross-lane traffic at all: the 16-word state,
 // the chaining value and the message block live in the lane's registers, and the sigma
 // schedule is resolved at compile time (every round fully unrolled), so a block costs the
@@ -1745,6 +1826,23 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   blake2b_kernel<kModeRefId><<<(unsigned)grid, kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out, hash_prio_blocks(),
       nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
+                       pfscdc_ref* refs, uint32_t* counter, hipStream_t st) {
+  if (max_segments == 0) return hipSuccess;
+  dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
+  return hipGetLastError();
+}
+
+hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pfscdc_segment* segs,
+                             const uint64_t* blk_base, uint32_t n, uint64_t nblocks,
+                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st) {
+  if (nblocks == 0) return hipSuccess;
+  const uint64_t need = (nblocks + 255) / 256, full = (uint64_t)num_cus * 32;
+  chacha_xor_kernel<<<(unsigned)(need < full ? need : full), 256, 0, st>>>(data, offs, segs,
+                                                                          blk_base, n, refs, out);
   return hipGetLastError();
 }
 

@@ -87,6 +87,11 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_ids;  // fill_synthetic_pieces
   DevBuf<uint64_t> d_starts;
   DevBuf<uint8_t> d_group, d_group_ct;  // writers_close_group: staged bytes, ciphertexts
+  DevBuf<pfscdc_segment> d_segs2;       // create_refs (split Ref.Id): records of the id pass
+  DevBuf<uint64_t> d_blk;               // create_refs (split): 64-B block prefix per record
+  DevBuf<uint8_t> d_ctext;              // create_refs (split): ciphertext when not asked for
+  PinnedBuf<uint64_t> h_blk;
+  PinnedBuf<pfscdc_segment> h_segs2;
   PinnedBuf<pfscdc_ref> h_refs;
   uint32_t options = 0;
   float get_ms = 0.f;
@@ -263,6 +268,11 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_starts.release();
   c->d_group.release();
   c->d_group_ct.release();
+  c->d_segs2.release();
+  c->d_blk.release();
+  c->d_ctext.release();
+  c->h_blk.release();
+  c->h_segs2.release();
   c->h_offs.release();
   c->h_seg_base.release();
   c->h_seg_begin.release();
@@ -938,6 +948,16 @@ int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
   return PFSCDC_OK;
 }
 
+// Split Ref.Id pass (ChaCha20 in parallel, then BLAKE2b of the ciphertext) when the chunk list
+// cannot fill the hash grid's quads, i.e. the pass is bound by its longest chains.
+// PFSCDC_REFID_SPLIT=0/1 forces either form (A/B and tests).
+static bool refid_split(uint32_t n, int num_cus) {
+  const char* e = getenv("PFSCDC_REFID_SPLIT");
+  if (e && *e) return atoi(e) != 0;
+  const uint64_t quads = (uint64_t)num_cus * 4 * kHashWavesPerSimd * 16;
+  return n <= quads;
+}
+
 // chunk.Create(ctx, CreateOptions{}, chunk, createFunc) for n chunks of a device buffer
 // (transform.go:26-46): dek = Hash(Hash(chunk)) (deriveKey :173-178), id = Hash(ChaCha20_dek
 // (chunk)) (cryptoXOR :181-188; the id the chunk client stores it under, client.go:57).
@@ -991,19 +1011,51 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, k, c->d_order.p,
                              c->d_qctr.p, c->num_cus, nbytes, st));
   HIP_OK(c, hipEventRecord(c->cev, st));
-  HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
-  HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
-                           c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st));
+  // Ref.Id = Hash(ChaCha20_dek(chunk)).  Fused (the quad computes each block's keystream on
+  // its BLAKE2b chain) when the chunks fill the GPU; split into a parallel ChaCha20 pass and
+  // a plain BLAKE2b pass over the ciphertext when they do not, so the serial chain of the
+  // longest chunk carries only BLAKE2b (about half the per-block latency).
+  uint8_t* ct = ctext_out;
+  bool split = refid_split(n, c->num_cus);
+  if (split && !ct) {
+    if (c->d_ctext.ensure(nbytes ? nbytes : 1) == hipSuccess) ct = c->d_ctext.p;
+    else split = false;  // no room for a ciphertext copy: the fused pass needs none
+  }
+  if (split) {
+    HIP_OK(c, c->h_blk.ensure(n + 1));
+    HIP_OK(c, c->d_blk.ensure(n + 1));
+    HIP_OK(c, c->d_segs2.ensure(n));
+    HIP_OK(c, c->h_segs2.ensure(n));
+    c->h_blk.p[0] = 0;
+    for (uint32_t r = 0; r < n; r++) c->h_blk.p[r + 1] = c->h_blk.p[r] + (c->h_segs.p[r].size + 63) / 64;
+    HIP_OK(c, hipMemcpyAsync(c->d_blk.p, c->h_blk.p, sizeof(uint64_t) * (n + 1),
+                             hipMemcpyHostToDevice, st));
+    HIP_OK(c, launch_deks(c->d_segs.p, c->d_counts.p + 2, n, c->d_refs.p, c->d_qctr.p + 1, st));
+    HIP_OK(c, launch_chacha_xor(data, c->d_offs.p, c->d_segs.p, c->d_blk.p, n, c->h_blk.p[n],
+                                c->d_refs.p, ct, c->num_cus, st));
+    HIP_OK(c, hipMemcpyAsync(c->d_segs2.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
+                             hipMemcpyDeviceToDevice, st));
+    HIP_OK(c, launch_blake2b(ct, c->d_offs.p, c->d_segs2.p, c->d_counts.p + 2, n, c->d_order.p,
+                             c->d_qctr.p + 1, c->num_cus, nbytes, st));
+  } else {
+    HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
+    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
+                             c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st));
+  }
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   if (hashes && k)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * k,
                              hipMemcpyDeviceToHost, st));
   HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, sizeof(pfscdc_ref) * n,
                            hipMemcpyDeviceToHost, st));
+  if (split)
+    HIP_OK(c, hipMemcpyAsync(c->h_segs2.p, c->d_segs2.p, sizeof(pfscdc_segment) * n,
+                             hipMemcpyDeviceToHost, st));
   HIP_OK(c, hipStreamSynchronize(st));
   for (uint32_t r = 0; r < n; r++) {
     const uint32_t i = c->perm[r];
     refs[i] = c->h_refs.p[r];
+    if (split) std::memcpy(refs[i].id, c->h_segs2.p[r].hash, 32);
     if (hashes && r < k) std::memcpy(hashes + 32ull * i, c->h_segs.p[r].hash, 32);
   }
   c->nsegs = 0;  // the scan results were overwritten

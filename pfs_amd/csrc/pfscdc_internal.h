@@ -110,6 +110,13 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
                           uint8_t* ctext_out, hipStream_t st);
+// dek per record (refs[].dek from segs[].hash); zeroes *counter
+hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
+                       pfscdc_ref* refs, uint32_t* counter, hipStream_t st);
+// out[range of record r] = ChaCha20_{refs[r].dek}(data[range]); blk_base: prefix of 64-B blocks
+hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pfscdc_segment* segs,
+                             const uint64_t* blk_base, uint32_t n, uint64_t nblocks,
+                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st);
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
                       int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st);

@@ -122,9 +122,13 @@ def test_get_chunks_device_resident_roundtrip_of_scan_refs():
 
 # ---------------------------------------------------------------- chunk formation + Create
 
-def test_create_refs_matches_oracle_with_known_hashes():
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_create_refs_matches_oracle_with_known_hashes(split, monkeypatch):
+    # split "1": ChaCha20 pass + BLAKE2b of the ciphertext; "0": the fused quad pass
+    monkeypatch.setenv("PFSCDC_REFID_SPLIT", split)
     rng = np.random.default_rng(21)
-    lens = [0, 1, 64, 127, 128, 129, 5000] + list(rng.integers(1, 400_000, 60))
+    lens = [0, 1, 63, 64, 65, 127, 128, 129, 5000, (3 << 20) + 5] + \
+        list(rng.integers(1, 400_000, 60))
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     data = synthetic_bytes(offs, 41)
     chunks = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
