@@ -21,13 +21,13 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;  // elements
-  hipError_t ensure(size_t n) {
+  hipError_t ensure(size_t n, bool exact = false) {
     if (n <= cap && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
-    want = want + want / 4;  // amortize growth
+    if (!exact) want = want + want / 4;  // amortize growth
     hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
     if (e == hipSuccess) cap = want;
     return e;
@@ -1018,8 +1018,17 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   uint8_t* ct = ctext_out;
   bool split = refid_split(n, c->num_cus);
   if (split && !ct) {
-    if (c->d_ctext.ensure(nbytes ? nbytes : 1) == hipSuccess) ct = c->d_ctext.p;
-    else split = false;  // no room for a ciphertext copy: the fused pass needs none
+    // a ciphertext copy of the whole input, only with room to spare (the fused pass needs
+    // none, and other contexts on the device need theirs)
+    size_t free_b = 0, total_b = 0;
+    if (c->d_ctext.cap < nbytes &&
+        (hipMemGetInfo(&free_b, &total_b) != hipSuccess ||
+         free_b + c->d_ctext.cap < nbytes + (8ull << 30)))
+      split = false;
+    else if (c->d_ctext.ensure(nbytes ? nbytes : 1, true) == hipSuccess)
+      ct = c->d_ctext.p;
+    else
+      split = false;
   }
   if (split) {
     HIP_OK(c, c->h_blk.ensure(n + 1));
