@@ -148,7 +148,11 @@ int pfscdc_last_get_ms(pfscdc_ctx* ctx, float* ms);
  * Ref.Dek = Hash(Hash(chunk)) and Ref.Id = Hash(ChaCha20_dek(chunk)).  content_hashes
  * (NULL or 32 B per chunk) is Hash(chunk) (chunkDataRef.Hash, writer.go:240): taken as
  * given where hash_known[i] != 0 (e.g. a single-DataRef chunk, whose hash the scan already
- * has), computed and written back otherwise.  Blocks until refs are on the host. */
+ * has), computed and written back otherwise.  Blocks until refs are on the host.
+ * The Ref.Id pass runs fused (keystream on the BLAKE2b chain) or split (a parallel ChaCha20
+ * pass into a ctx-owned ciphertext copy, then BLAKE2b of it) when nchunks cannot fill the
+ * GPU and 8 GiB of device memory stay free; the environment variable PFSCDC_REFID_SPLIT=0/1
+ * forces either.  Same results either way. */
 int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
                        const uint8_t* hash_known, pfscdc_ref* refs);
@@ -157,7 +161,7 @@ int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
 int pfscdc_hash_data_refs(pfscdc_ctx* ctx, const uint8_t* hashes, uint32_t n, uint8_t out[32]);
 /* Device time (ms) of the last chunk.Create batch (pfscdc_create_refs or a writer flush). */
 int pfscdc_last_create_ms(pfscdc_ctx* ctx, float* ms);
-/* Its split: out[0] content-hash pass, out[1] Ref.Id pass (order, dek, ChaCha20 + BLAKE2b). */
+/* Its split: out[0] content-hash pass, out[1] Ref.Id pass (dek, ChaCha20, BLAKE2b). */
 int pfscdc_last_create_timings(pfscdc_ctx* ctx, float out[2]);
 
 /* ---- one stream split across GPUs (writer.go:163-189 block-parallel) --------
