@@ -1147,6 +1147,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   const uint64_t iv_c = pick4(j, kB2IV[0], kB2IV[1], kB2IV[2], kB2IV[3]);
   const uint64_t iv_d = pick4(j, kB2IV[4], kB2IV[5], kB2IV[6], kB2IV[7]);
   const uint64_t h0a = j == 0 ? (kB2IV[0] ^ 0x01010020ULL) : iv_c;  // digest 32, fanout/depth 1
+  const uint64_t t_mask = j == 0 ? ~0ULL : 0ULL;  // the byte counter t goes into v[12] (lane 0)
   const uint64_t h0b = iv_d;
 
   if ((prio_blocks >> 31) && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // A/B: static
@@ -1200,8 +1201,14 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
 
   auto step = [&](auto par) -> bool {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
+    // fast (wave-uniform): a quiet block in which every active quad is at least 4 blocks from
+    // its end (after the decrement, the shortest active chain has quiet + 1 blocks left), so
+    // no block is the last, and the block fetched at round 5 is a full one: the per-block
+    // bookkeeping reduces to straight-line code (no per-lane last/tail selects or branches).
+    bool fast = false;
     if (quiet) {
       quiet--;
+      fast = quiet >= 3;
     } else {
       if (!drained) {
         const bool need = !active;
@@ -1264,7 +1271,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       }
       quiet = graded ? 0u : q;
     }
-    const bool last = blk + 1 == nblk;
+    const bool last = !fast && blk + 1 == nblk;
     if (MODE == kModeRefId) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1295,9 +1302,13 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint64_t x0 = lds_abs_u64(ma[0][0] + cur), x1 = lds_abs_u64(ma[0][1] + cur);
     uint64_t x2 = lds_abs_u64(ma[0][2] + cur), x3 = lds_abs_u64(ma[0][3] + cur);
-    const uint64_t t = last ? L : (blk + 1) * 128;
-    uint64_t a = ha, b = hb, c = iv_c;
-    uint64_t d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
+    uint64_t a = ha, b = hb, c = iv_c, d;
+    if (fast) {
+      d = iv_d ^ (((blk + 1) << 7) & t_mask);
+    } else {
+      const uint64_t t = last ? L : (blk + 1) * 128;
+      d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
+    }
 #pragma unroll
     for (int r = 0; r < 12; r++) {
       uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
@@ -1350,7 +1361,9 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       store_block(cur);
     }
-    if (active) {
+    if (fast) {
+      blk++;  // inactive quads too: a refill resets blk
+    } else if (active) {
       blk++;
       if (last) {  // digest = h[0..3] little endian; lane j owns h[j]
         if (MODE == kModeRefId) reinterpret_cast<uint64_t*>(refs[sidx].id)[j] = ha;
