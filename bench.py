@@ -106,6 +106,8 @@ def parse():
                     help="c2: configs[1] batches in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-chain-floor", action="store_true",
+                    help="skip the one-chain rate measurement (chain_floor)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="c2: skip the two-in-flight throughput leg")
     ap.add_argument("--no-literal", action="store_true",
@@ -532,6 +534,8 @@ def main():
     del batches[1:]
     torch.cuda.empty_cache()
 
+    if rank == 0 and world == 1 and not args.no_chain_floor:
+        out["chain_floor"] = chain_floor(res, hash_ms, data, params, local, Chunker)
     if rank == 0 and world == 1 and args.config == "c2" and S == 1 and not args.no_pipelined:
         out["two_in_flight"] = two_in_flight(args, work, chunker, data, params, local, Chunker,
                                              torch)
@@ -548,6 +552,30 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     chunker.close()
+
+
+def chain_floor(res, hash_ms, data, params, local, Chunker):
+    """The BLAKE2b per-segment latency bound: a segment is one serial chain, so
+    no hash launch can end before its longest segment, hashed alone at one quad's rate.  The
+    rate is measured here on one 8 MiB range of the step's input, alone on the GPU."""
+    longest = int(res.segments["size"].max()) if len(res.segments) else 0
+    n = min(8 << 20, int(data.numel()))
+    c = Chunker(params, device=local)
+    c.hash_ranges(data, [0], [n])  # warm
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        c.hash_ranges(data, [0], [n])
+        ts.append(time.perf_counter() - t0)
+    c.close()
+    rate = n / min(ts)
+    floor_ms = longest / rate * 1e3
+    return {"longest_segment_bytes": longest, "one_chain_MB_per_s": round(rate / 1e6, 1),
+            "floor_ms": round(floor_ms, 2),
+            "hash_ms": round(hash_ms, 3) if hash_ms else None,
+            "hash_over_floor": round(hash_ms / floor_ms, 3) if hash_ms and floor_ms else None,
+            "note": "floor = longest segment / one chain's rate (one quad alone, 8 MiB range of "
+                    "this input, best of 3 incl. launch); the hash launch cannot end earlier"}
 
 
 def two_in_flight(args, work, chunker, data, params, local, Chunker, torch):

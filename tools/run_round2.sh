@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out && export TMPDIR=/tmp
-B="--no-cpu-baseline --no-e2e --no-literal --no-pipelined"
+B="--no-cpu-baseline --no-e2e --no-literal --no-pipelined --no-chain-floor"
 timeout -k 10 120 ./tools/valu_issue > gpurun_out/valu_issue.txt 2>&1 && \
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_gpu.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
