@@ -1199,6 +1199,64 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     }
   };
 
+  // The 12 rounds of one block from LDS buffer `par` (state in a, b, c, d, column layout in
+  // and out); at round 5, put_next() stages the quad's next block in the other buffer.
+  auto rounds = [&](auto par, uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
+                    auto&& put_next) {
+    constexpr uint32_t cur = decltype(par)::value * kMsgBuf;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint64_t x0 = lds_abs_u64(ma[0][0] + cur), x1 = lds_abs_u64(ma[0][1] + cur);
+    uint64_t x2 = lds_abs_u64(ma[0][2] + cur), x3 = lds_abs_u64(ma[0][3] + cur);
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+      uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+      if (r < 11) {
+        y0 = lds_abs_u64(ma[r + 1][0] + cur);
+        y1 = lds_abs_u64(ma[r + 1][1] + cur);
+        y2 = lds_abs_u64(ma[r + 1][2] + cur);
+        y3 = lds_abs_u64(ma[r + 1][3] + cur);
+      }
+#ifdef PFS_HASH_CXX
+      PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
+      a = quad_perm64<0x93>(a);            // a <- v[(j+3)%4]
+      c = quad_perm64<0x39>(c);            // c <- v[8+(j+1)%4]
+      d = quad_perm64<0x4E>(d);            // d <- v[12+(j+2)%4]
+      PFS_G(a, b, c, d, x2, x3);           // diagonal step through b_j: G_{4+(j+3)%4}
+      a = quad_perm64<0x39>(a);
+      c = quad_perm64<0x93>(c);
+      d = quad_perm64<0x4E>(d);
+#else
+      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves a, c, d in the diagonal layout
+#endif
+      x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+      if (r == 5) put_next();
+    }
+#ifndef PFS_HASH_CXX
+    a = quad_perm64<0x39>(a);  // back to the column layout
+    c = quad_perm64<0x93>(c);
+    d = quad_perm64<0x4E>(d);
+#endif
+  };
+
+  // A block in a run of quiet blocks (content hash only): every active quad is at least 4
+  // blocks from its end, so nothing in it depends on a lane's position in its chain.  Runs
+  // of these execute in their own loop, straight-line code between the round blocks.
+  auto fast_step = [&](auto par) {
+    constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
+    uint64_t a = ha, b = hb, c = iv_c, d = iv_d ^ (((blk + 1) << 7) & t_mask);
+    rounds(par, a, b, c, d, [&] {
+      if (active) {
+        lds_put(nxt);
+        msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
+      }
+    });
+    ha ^= a ^ c;
+    hb ^= b ^ d;
+    blk++;  // inactive quads too: a refill resets blk
+  };
+
   auto step = [&](auto par) -> bool {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     // fast (wave-uniform): a quiet block in which every active quad is at least 4 blocks from
@@ -1297,11 +1355,6 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         store_block(cur);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint64_t x0 = lds_abs_u64(ma[0][0] + cur), x1 = lds_abs_u64(ma[0][1] + cur);
-    uint64_t x2 = lds_abs_u64(ma[0][2] + cur), x3 = lds_abs_u64(ma[0][3] + cur);
     uint64_t a = ha, b = hb, c = iv_c, d;
     if (fast) {
       d = iv_d ^ (((blk + 1) << 7) & t_mask);
@@ -1309,38 +1362,12 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       const uint64_t t = last ? L : (blk + 1) * 128;
       d = iv_d ^ (j == 0 ? t : 0) ^ ((j == 2 && last) ? ~0ULL : 0);
     }
-#pragma unroll
-    for (int r = 0; r < 12; r++) {
-      uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
-      if (r < 11) {
-        y0 = lds_abs_u64(ma[r + 1][0] + cur);
-        y1 = lds_abs_u64(ma[r + 1][1] + cur);
-        y2 = lds_abs_u64(ma[r + 1][2] + cur);
-        y3 = lds_abs_u64(ma[r + 1][3] + cur);
-      }
-#ifdef PFS_HASH_CXX
-      PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
-      a = quad_perm64<0x93>(a);            // a <- v[(j+3)%4]
-      c = quad_perm64<0x39>(c);            // c <- v[8+(j+1)%4]
-      d = quad_perm64<0x4E>(d);            // d <- v[12+(j+2)%4]
-      PFS_G(a, b, c, d, x2, x3);           // diagonal step through b_j: G_{4+(j+3)%4}
-      a = quad_perm64<0x39>(a);
-      c = quad_perm64<0x93>(c);
-      d = quad_perm64<0x4E>(d);
-#else
-      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves a, c, d in the diagonal layout
-#endif
-      x0 = y0; x1 = y1; x2 = y2; x3 = y3;
-      if (r == 5 && active && !last) {  // block blk+1 -> the other buffer; fetch blk+2
+    rounds(par, a, b, c, d, [&] {
+      if (active && !last) {  // block blk+1 -> the other buffer; fetch blk+2
         lds_put(nxt);
         if (blk + 2 < nblk) load_block(blk + 2);
       }
-    }
-#ifndef PFS_HASH_CXX
-    a = quad_perm64<0x39>(a);  // back to the column layout
-    c = quad_perm64<0x93>(c);
-    d = quad_perm64<0x4E>(d);
-#endif
+    });
     ha ^= a ^ c;
     hb ^= b ^ d;
     if (MODE == kModeGet) {  // decrypt the hashed ciphertext block in place, store plaintext
@@ -1373,7 +1400,27 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     }
     return true;
   };
-  while (step(std::integral_constant<uint32_t, 0>{}) && step(std::integral_constant<uint32_t, 1>{})) {
+  constexpr std::integral_constant<uint32_t, 0> P0{};
+  constexpr std::integral_constant<uint32_t, 1> P1{};
+  // quiet counts blocks still free of bookkeeping; a block with quiet = Q before it has every
+  // active quad at least Q blocks from its end, so pairs of fast blocks need Q >= 5
+  while (true) {
+    if (!step(P0)) break;
+    if constexpr (MODE == kModeHash) {
+      while (quiet >= 5) {
+        fast_step(P1);
+        fast_step(P0);
+        quiet -= 2;
+      }
+    }
+    if (!step(P1)) break;
+    if constexpr (MODE == kModeHash) {
+      while (quiet >= 5) {
+        fast_step(P0);
+        fast_step(P1);
+        quiet -= 2;
+      }
+    }
   }
   span_end(span);
 }
