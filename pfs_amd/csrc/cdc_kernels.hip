@@ -1404,15 +1404,10 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   constexpr std::integral_constant<uint32_t, 1> P1{};
   // quiet counts blocks still free of bookkeeping; a block with quiet = Q before it has every
   // active quad at least Q blocks from its end, so pairs of fast blocks need Q >= 5
+  // (one copy of the fast loop, entered after a parity-1 step: one hot loop body in the
+  // instruction cache)
   while (true) {
     if (!step(P0)) break;
-    if constexpr (MODE == kModeHash) {
-      while (quiet >= 5) {
-        fast_step(P1);
-        fast_step(P0);
-        quiet -= 2;
-      }
-    }
     if (!step(P1)) break;
     if constexpr (MODE == kModeHash) {
       while (quiet >= 5) {
