@@ -187,3 +187,27 @@ def test_digests_are_blake2b_of_segment_bytes():
         a = int(offs[s["file"]] + s["offset"])
         want = hashlib.blake2b(data[a:a + int(s["size"])].tobytes(), digest_size=32).digest()
         assert bytes(s["hash"]) == want
+
+
+def test_hash_chain_ends_around_the_quiet_thresholds():
+    """The hash kernel runs blocks of a wave's quiet stretch in a separate straight-line loop
+    (pairs of blocks while every active quad is >= 5 blocks from its chain's end) and the
+    general step otherwise.  Chains whose ends fall 0..40 blocks apart, in waves of 16 quads,
+    with partial last blocks, cross every threshold; one quad per wave left alone at the end
+    covers the masked fetch for idle quads.  Digests against hashlib (BLAKE2b-256)."""
+    rng = np.random.default_rng(77)
+    sizes = []
+    for base in (1, 4, 5, 6, 9, 64, 300):
+        for k in range(48):
+            sizes.append(128 * (base + k % 41) + int(rng.integers(0, 128)))
+    sizes += [128 * 2000 + 5]  # a long lone chain after the others end
+    sizes = np.array(sizes, dtype=np.uint64)
+    begins = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 0x51)
+    ch = Chunker(ChunkParams(), 0)
+    got = ch.hash_ranges(data, begins, sizes)
+    for i in range(len(sizes)):
+        a, n = int(begins[i]), int(sizes[i])
+        want = hashlib.blake2b(data[a:a + n].tobytes(), digest_size=32).digest()
+        assert bytes(got[i]) == want, f"range {i} ({n} B)"
