@@ -492,6 +492,7 @@ def main():
                 "(first wavefront start to last wavefront end); the hash is VALU-issue bound, "
                 "not HBM bound (DESIGN.md §4)",
         "cdc_only_gib_s": round(total / (scan_ms * 1e-3) / GIB, 2) if scan_ms else None,
+        "hash_only_gib_s": round(total / (hash_ms * 1e-3) / GIB, 2) if hash_ms else None,
         "roofline": roofline,
         "roofline_cdc": roofline_cdc,
     }
