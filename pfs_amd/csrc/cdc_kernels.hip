@@ -1201,14 +1201,21 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
 
   // The 12 rounds of one block from LDS buffer `par` (state in a, b, c, d, column layout in
   // and out); at round 5, put_next() stages the quad's next block in the other buffer.
+  // pre (optional): round 0's message words, already read (the quiet-run loop reads the next
+  // block's at round 11 into pre, from the buffer round 5 staged it in).
   auto rounds = [&](auto par, uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
-                    auto&& put_next) {
-    constexpr uint32_t cur = decltype(par)::value * kMsgBuf;
+                    auto&& put_next, uint64_t* pre = nullptr) {
+    constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint64_t x0 = lds_abs_u64(ma[0][0] + cur), x1 = lds_abs_u64(ma[0][1] + cur);
-    uint64_t x2 = lds_abs_u64(ma[0][2] + cur), x3 = lds_abs_u64(ma[0][3] + cur);
+    uint64_t x0, x1, x2, x3;
+    if (pre) {
+      x0 = pre[0]; x1 = pre[1]; x2 = pre[2]; x3 = pre[3];
+    } else {
+      x0 = lds_abs_u64(ma[0][0] + cur); x1 = lds_abs_u64(ma[0][1] + cur);
+      x2 = lds_abs_u64(ma[0][2] + cur); x3 = lds_abs_u64(ma[0][3] + cur);
+    }
 #pragma unroll
     for (int r = 0; r < 12; r++) {
       uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
@@ -1217,6 +1224,14 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         y1 = lds_abs_u64(ma[r + 1][1] + cur);
         y2 = lds_abs_u64(ma[r + 1][2] + cur);
         y3 = lds_abs_u64(ma[r + 1][3] + cur);
+      } else if (pre) {  // the next block's round 0, staged at round 5 in the other buffer
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pre[0] = lds_abs_u64(ma[0][0] + nxt);
+        pre[1] = lds_abs_u64(ma[0][1] + nxt);
+        pre[2] = lds_abs_u64(ma[0][2] + nxt);
+        pre[3] = lds_abs_u64(ma[0][3] + nxt);
       }
 #ifdef PFS_HASH_CXX
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
@@ -1243,7 +1258,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // A block in a run of quiet blocks (content hash only): every active quad is at least 4
   // blocks from its end, so nothing in it depends on a lane's position in its chain.  Runs
   // of these execute in their own loop, straight-line code between the round blocks.
-  auto fast_step = [&](auto par) {
+  auto fast_step = [&](auto par, uint64_t* pre) {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     uint64_t a = ha, b = hb, c = iv_c, d = iv_d ^ (((blk + 1) << 7) & t_mask);
     rounds(par, a, b, c, d, [&] {
@@ -1251,7 +1266,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         lds_put(nxt);
         msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
       }
-    });
+    }, pre);
     ha ^= a ^ c;
     hb ^= b ^ d;
     blk++;  // inactive quads too: a refill resets blk
@@ -1410,10 +1425,14 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     if (!step(P0)) break;
     if (!step(P1)) break;
     if constexpr (MODE == kModeHash) {
-      while (quiet >= 5) {
-        fast_step(P0);
-        fast_step(P1);
-        quiet -= 2;
+      if (quiet >= 5) {
+        uint64_t pre[4] = {lds_abs_u64(ma[0][0]), lds_abs_u64(ma[0][1]), lds_abs_u64(ma[0][2]),
+                           lds_abs_u64(ma[0][3])};  // buffer 0 (P0): the next block
+        do {
+          fast_step(P0, pre);
+          fast_step(P1, pre);
+          quiet -= 2;
+        } while (quiet >= 5);
       }
     }
   }
