@@ -1852,30 +1852,48 @@ static uint32_t hash_prio_blocks() {
   return v;
 }
 
+// Waves per SIMD for a hash launch.  One quad runs a chain's 128-B blocks strictly in order,
+// so no launch ends before its longest chain; a second wave on a SIMD only slows that chain
+// down (the two share the issue slots).  One wave per SIMD when the launch is bound by its
+// longest chain even then (longest blocks >= total blocks / the quads of one wave per SIMD:
+// c3, c4, a single configs[1] batch, most chunk.Create passes), two otherwise (c2's 128 GiB
+// steps: 72 vs 80 ms; c4: 100 vs 104-110 ms).  PFSCDC_HASH_WAVES=n forces n (A/B).
+int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus) {
+  static const int forced = [] {
+    const char* e = getenv("PFSCDC_HASH_WAVES");
+    const int w = e ? atoi(e) : 0;
+    return w >= 1 && w <= 8 ? w : 0;
+  }();
+  if (forced) return forced;
+  const uint64_t quads1 = (uint64_t)num_cus * 4 * (64 / 4);
+  const uint64_t longest = (longest_bytes + 127) / 128, total = total_bytes / 128;
+  return longest * quads1 >= total ? 1 : kHashWavesPerSimd;
+}
+
+static unsigned hash_grid(uint64_t max_segments, int num_cus, int waves) {
+  const uint64_t quads_per_block = kHashBlock / 4;
+  const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
+  const uint64_t full = (uint64_t)num_cus * 4 * (waves > 0 ? waves : kHashWavesPerSimd) /
+                        (kHashBlock / 64);
+  return (unsigned)(need < full ? need : full);
+}
+
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
-                          bool ordered, uint64_t* span) {
+                          bool ordered, uint64_t* span, int waves) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
-  static const int waves_per_simd = [] {  // tuning knob (PFSCDC_HASH_WAVES), default 2
-    const char* e = getenv("PFSCDC_HASH_WAVES");
-    const int w = e ? atoi(e) : kHashWavesPerSimd;
-    return w >= 1 && w <= 8 ? w : kHashWavesPerSimd;
-  }();
   if (kHashLanesPerSegment == 1) {
     const uint64_t need = (max_segments + kHashLaneBlock - 1) / kHashLaneBlock;
-    const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashLaneBlock / 64);
+    const uint64_t full = (uint64_t)num_cus * 4 * (waves > 0 ? waves : kHashWavesPerSimd) /
+                          (kHashLaneBlock / 64);
     const uint64_t grid = need < full ? need : full;
     blake2b_lane_kernel<<<(unsigned)grid, kHashLaneBlock, 0, st>>>(data, offs, segs, seg_count,
                                                                    order, counter, nbytes);
     return hipGetLastError();
   }
-  const uint64_t quads_per_block = kHashBlock / 4;
-  const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
-  const uint64_t full = (uint64_t)num_cus * 4 * waves_per_simd / (kHashBlock / 64);
-  const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<kModeHash><<<(unsigned)grid, kHashBlock, 0, st>>>(
+  blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr, hash_prio_blocks(),
       span);
   return hipGetLastError();
@@ -1890,14 +1908,10 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st) {
+                          uint8_t* ctext_out, hipStream_t st, int waves) {
   if (max_segments == 0) return hipSuccess;
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
-  const uint64_t quads_per_block = kHashBlock / 4;
-  const uint64_t need = (max_segments + quads_per_block - 1) / quads_per_block;
-  const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
-  const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<kModeRefId><<<(unsigned)grid, kHashBlock, 0, st>>>(
+  blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out, hash_prio_blocks(),
       nullptr);
   return hipGetLastError();
@@ -1922,14 +1936,11 @@ hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pf
 
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
-                      int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st) {
+                      int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st,
+                      int waves) {
   if (nsegs == 0) return hipSuccess;
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
-  const uint64_t quads_per_block = kHashBlock / 4;
-  const uint64_t need = (nsegs + quads_per_block - 1) / quads_per_block;
-  const uint64_t full = (uint64_t)num_cus * 4 * kHashWavesPerSimd / (kHashBlock / 64);
-  const uint64_t grid = need < full ? need : full;
-  blake2b_kernel<kModeGet><<<(unsigned)grid, kHashBlock, 0, st>>>(
+  blake2b_kernel<kModeGet><<<hash_grid(nsegs, num_cus, waves), kHashBlock, 0, st>>>(
       ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
       nullptr);
   return hipGetLastError();

@@ -340,12 +340,16 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->h_offs.ensure(nfiles + 1));
   HIP_OK(c, c->h_seg_base.ensure(nfiles + 1));
   std::memcpy(c->h_offs.p, file_offsets, sizeof(uint64_t) * (nfiles + 1));
-  uint64_t cap = 0;
+  uint64_t cap = 0, longest_file = 0;
   for (uint32_t f = 0; f < nfiles; f++) {
     c->h_seg_base.p[f] = cap;
     const uint64_t len = file_offsets[f + 1] - file_offsets[f];
     cap += len ? len / (uint64_t)p.min_chunk + 1 : 0;
+    longest_file = std::max(longest_file, len);
   }
+  // the hash's longest chain is at most the largest file and at most max_chunk
+  const int waves = hash_waves(std::min<uint64_t>(longest_file, (uint64_t)p.max_chunk), nbytes,
+                               c->num_cus);
   c->h_seg_base.p[nfiles] = cap;
   c->slot_cap = cap;
   c->nfiles = nfiles;
@@ -416,13 +420,13 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
-                             c->d_span.p + 2));
+                             c->d_span.p + 2, waves));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p,
-                             nullptr, st));
+                             nullptr, st, waves));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)
@@ -602,8 +606,11 @@ int pfscdc_get_chunks(pfscdc_ctx* c, const void* ctext, uint64_t nbytes, int cte
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, hipEventRecord(c->ev[7], st));
+  uint64_t longest = 0;
+  for (uint32_t i = 0; i < nchunks; i++) longest = std::max(longest, c->h_segs.p[i].size);
   HIP_OK(c, launch_get(in, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, nchunks, c->d_order.p,
-                       c->d_qctr.p, c->num_cus, nbytes, c->d_refs.p, outp, st));
+                       c->d_qctr.p, c->num_cus, nbytes, c->d_refs.p, outp, st,
+                       hash_waves(longest, nbytes, c->num_cus)));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * nchunks,
                            hipMemcpyDeviceToHost, st));
@@ -678,7 +685,7 @@ int pfscdc_hash_data_refs(pfscdc_ctx* c, const uint8_t* hashes, uint32_t n, uint
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, launch_blake2b(c->d_data.p, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, 1,
-                           c->d_order.p, c->d_qctr.p, c->num_cus, nb, st));
+                           c->d_order.p, c->d_qctr.p, c->num_cus, nb, st, false, nullptr, 1));
   HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment), hipMemcpyDeviceToHost, st));
   HIP_OK(c, hipStreamSynchronize(st));
   std::memcpy(out, c->h_segs.p[0].hash, 32);
@@ -937,8 +944,14 @@ int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
+  uint64_t longest = 0, sum = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    longest = std::max(longest, sizes[i]);
+    sum += sizes[i];
+  }
   HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, n, c->d_order.p,
-                           c->d_qctr.p, c->num_cus, nbytes, st));
+                           c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
+                           hash_waves(longest, sum, c->num_cus)));
   HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
                            hipMemcpyDeviceToHost, st));
   HIP_OK(c, hipStreamSynchronize(st));
@@ -1006,10 +1019,21 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, 2 * sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
+  uint64_t longest_k = 0, sum_k = 0, longest_n = 0, sum_n = 0;
+  for (uint32_t r = 0; r < n; r++) {
+    const uint64_t z = c->h_segs.p[r].size;
+    if (r < k) {
+      longest_k = std::max(longest_k, z);
+      sum_k += z;
+    }
+    longest_n = std::max(longest_n, z);
+    sum_n += z;
+  }
   HIP_OK(c, hipEventRecord(c->ev[7], st));
   if (k)
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, k, c->d_order.p,
-                             c->d_qctr.p, c->num_cus, nbytes, st));
+                             c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
+                             hash_waves(longest_k, sum_k, c->num_cus)));
   HIP_OK(c, hipEventRecord(c->cev, st));
   // Ref.Id = Hash(ChaCha20_dek(chunk)).  Fused (the quad computes each block's keystream on
   // its BLAKE2b chain) when the chunks fill the GPU; split into a parallel ChaCha20 pass and
@@ -1045,11 +1069,13 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
     HIP_OK(c, hipMemcpyAsync(c->d_segs2.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
                              hipMemcpyDeviceToDevice, st));
     HIP_OK(c, launch_blake2b(ct, c->d_offs.p, c->d_segs2.p, c->d_counts.p + 2, n, c->d_order.p,
-                             c->d_qctr.p + 1, c->num_cus, nbytes, st));
+                             c->d_qctr.p + 1, c->num_cus, nbytes, st, false, nullptr,
+                             hash_waves(longest_n, sum_n, c->num_cus)));
   } else {
     HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
-                             c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st));
+                             c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st,
+                             hash_waves(longest_n, sum_n, c->num_cus)));
   }
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   if (hashes && k)

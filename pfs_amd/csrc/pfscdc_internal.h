@@ -103,13 +103,15 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
-                          bool ordered = false, uint64_t* span = nullptr);
+                          bool ordered = false, uint64_t* span = nullptr, int waves = 0);
+// waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all
+int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
                         uint32_t* counter, hipStream_t st);
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st);
+                          uint8_t* ctext_out, hipStream_t st, int waves = 0);
 // dek per record (refs[].dek from segs[].hash); zeroes *counter
 hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
                        pfscdc_ref* refs, uint32_t* counter, hipStream_t st);
@@ -119,7 +121,8 @@ hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pf
                              const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st);
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
-                      int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st);
+                      int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st,
+                      int waves = 0);
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, const uint32_t* ids,
                         const uint64_t* starts, uint64_t seed, uint32_t mode, hipStream_t st);
 
