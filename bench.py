@@ -427,11 +427,12 @@ def main():
              for name in steps_t[0]} if steps_t else {}
     tj = load_traffic(args, work)
 
-    def roof(ms, kernel, traffic_key=None):
-        ach = total / (ms * 1e-3) / 1e9 if ms and ms > 0 else 0.0
+    def roof(ms, kernel, traffic_key=None, nbytes=None):
+        nbytes = total if nbytes is None else nbytes
+        ach = nbytes / (ms * 1e-3) / 1e9 if ms and ms > 0 else 0.0
         r = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-             "bytes_per_launch": total, "avg_launch_ms": round(ms, 4) if ms else None,
+             "bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 4) if ms else None,
              "kernel": kernel}
         if tj and traffic_key and tj.get(traffic_key):
             r["traffic"] = tj[traffic_key]
@@ -453,8 +454,16 @@ def main():
     if args.ref_ids and kmean.get("ref_ids", 0) > (hash_ms or 0):
         roofline = roof(kmean["ref_ids"], "blake2b_kernel<kModeRefId> (ChaCha20 + BLAKE2b of "
                                           "the ciphertext; HIP events)")
+    # the scan rolls only the bytes that can hold a cut (the first min - 1 bytes of a file
+    # never do: writer.go:167-170), so its per-launch bytes are the rolled ones
+    try:
+        rolled = chunkers[0].last_scan_bytes()
+    except Exception:  # noqa: BLE001 - a path without a batch scan
+        rolled = total
     roofline_cdc = roof(scan_ms, "cdc_scan_kernel (its last workgroup compacts the candidates)",
-                        "cdc_scan_kernel")
+                        "cdc_scan_kernel", nbytes=rolled)
+    roofline_cdc["file_bytes_per_launch"] = total
+    roofline_cdc["rolled_fraction"] = round(rolled / total, 5) if total else None
     rvalu = {}
     if tj:
         for kern, ms in (("blake2b_kernel", hash_ms), ("cdc_scan_kernel", scan_ms)):

@@ -193,6 +193,13 @@ int pfscdc_hash_ranges(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
  * hook for the candidate-scan kernel. */
 uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
 
+/* Bytes the last pfscdc_scan's candidate kernel actually rolled.  Writer.roll never cuts in
+ * the first min - 1 bytes after an Annotate (writer.go:125-128,167-170), so the scan skips
+ * that part of every file (in 8 KiB steps of its work units) and the count is below nbytes
+ * when files are longer than min; results are unchanged.  PFSCDC_SCAN_SKIP=0 (environment)
+ * rolls every byte. */
+int pfscdc_last_scan_bytes(pfscdc_ctx* ctx, uint64_t* out);
+
 /* Device timing of the last scan's kernels (ms, HIP events on the ctx stream):
  * out[0] candidate scan (its last workgroup also compacts the candidates), out[1] 0 (the
  * compaction used to be a launch of its own), out[2] selection (its last workgroup also

@@ -32,6 +32,7 @@ EXPORTED = [
     "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
+    "pfscdc_last_scan_bytes",
     "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms", "pfscdc_get_chunks",
     "pfscdc_last_get_ms",
     "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
@@ -176,6 +177,7 @@ def load() -> C.CDLL:
             "pfscdc_file_segment_begin": (P(u64), [vp]),
             "pfscdc_debug_candidates": (u64, [vp, P(u64), u64]),
             "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
+            "pfscdc_last_scan_bytes": (i32, [vp, P(u64)]),
             "pfscdc_last_kernel_spans": (i32, [vp, P(C.c_float)]),
             "pfscdc_set_options": (i32, [vp, u32]),
             "pfscdc_refs": (vp, [vp]),

@@ -321,6 +321,13 @@ class Chunker:
         self._arg_keep = arr
         return (arr.ctypes.data if arr.size else None), arr.size, 0
 
+    def last_scan_bytes(self) -> int:
+        """Bytes the last scan's candidate kernel rolled (the first min - 1 bytes of each file
+        hold no cut point and are skipped; pfscdc_last_scan_bytes)."""
+        v = C.c_uint64(0)
+        self._check(self.lib.pfscdc_last_scan_bytes(self.ctx, C.byref(v)), "last_scan_bytes")
+        return int(v.value)
+
     def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
         out = (C.c_uint64 * cap)()
         n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)

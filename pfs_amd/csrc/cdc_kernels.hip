@@ -354,7 +354,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr, uint32_t* __restrict__ done_ctr,
-    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries, uint64_t* span) {
+    uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries,
+    const uint32_t* __restrict__ unit_skip, uint64_t* span) {
   span_begin(span);
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
   // images.  recs[] is zeroed before the launch; candidates are added to it directly.
@@ -375,13 +376,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   uint8_t* wbuf = smem + kTableLdsBytes + wave * kStageBytes;
   const uint32_t rd_base = lane * 128u;
   const uint32_t swz_l = stage_swz(lane);
-  // this lane's DMA piece in instruction i: row r_i = 8i + lane/8, chunk (lane%8) ^ swz(r_i)
-  uint32_t dma_off[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t r = 8u * i + (lane >> 3);
-    dma_off[i] = r * kStrip + 16u * ((lane & 7u) ^ stage_swz(r));
-  }
   __syncthreads();  // table copies written; from here on every wave runs on its own
 
 #if PFS_SCAN_DYN
@@ -402,9 +396,22 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
 #endif
     TileRec* const rec = recs + tile;
     const uint64_t tile_base = tile * kTile;
-    const uint64_t wave_base = tile_base + wslot * 64 * kStrip;
-    if (wave_base < n) {  // wave-uniform
-      const bool fast = wave_base + 64 * (uint64_t)kStrip <= n_main;
+    // Leading 128-byte steps of this unit's strips that hold no eligible position (inside
+    // the first min - 1 bytes of a file: scan_skip_kernel); the strips then shrink to cover
+    // the rest of the unit.  kStrip / 128 = the whole unit is skipped.
+    const uint32_t skip =
+        unit_skip ? (uint32_t)__builtin_amdgcn_readfirstlane((int)unit_skip[tile * kScanWaves + wslot]) : 0u;
+    const uint32_t nsteps = kStrip / 128 - skip, strip = nsteps * 128u;
+    const uint64_t wave_base = tile_base + wslot * 64 * kStrip + (uint64_t)skip * (64 * 128);
+    if (nsteps && wave_base < n) {  // wave-uniform
+      // this lane's DMA piece in instruction i: row r_i = 8i + lane/8, chunk (lane%8) ^ swz(r_i)
+      uint32_t dma_off[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t r = 8u * i + (lane >> 3);
+        dma_off[i] = r * strip + 16u * ((lane & 7u) ^ stage_swz(r));
+      }
+      const bool fast = wave_base + 64 * (uint64_t)strip <= n_main;
       auto dma_step = [&](uint32_t step) {
         if (fast) {  // wave-uniform: a scalar base plus the lane's 32-bit offset, LDS dst in M0
           const uint8_t* base = data + (wave_base + step * 128u);
@@ -423,7 +430,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
               (__attribute__((address_space(3))) void*)(wbuf + i * 1024), 16, 0, 0);
         }
       };
-      const uint64_t s0 = wave_base + (uint64_t)lane * kStrip;
+      const uint64_t s0 = wave_base + (uint64_t)lane * strip;
       dma_step(0);
       uint32_t prv[16], cur[32];
       if (s0 >= 64 && s0 - 64 < n) {
@@ -449,7 +456,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
       // position is a candidate iff (G_lo ^ ring) < 2^kshift, and the block test is a min
       const uint32_t cand_thr = 1u << kshift;
       const bool active = s0 < n;
-      for (uint32_t step = 0; step < kStrip / 128; step++) {
+      for (uint32_t step = 0; step < nsteps; step++) {
 #ifndef PFS_EXP_NO_DMA_WAIT
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's DMA has landed
 #endif
@@ -464,7 +471,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): row is in registers (WAR vs DMA)
         __builtin_amdgcn_wave_barrier();
-        if (step + 1 < kStrip / 128) dma_step(step + 1);    // refill while we compute
+        if (step + 1 < nsteps) dma_step(step + 1);    // refill while we compute
         const uint64_t pos = s0 + step * 128u;
         if (active && pos < n) {
           uint32_t* c0 = cur;
@@ -493,6 +500,60 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
       compact_tiles<kScanBlock>(recs, ntiles, n, entries, n_entries, s_wave);
   }
   span_end(span);
+}
+
+// Which leading part of each scan work unit (a wave's 64 strips, 64 * kStrip bytes) can hold
+// no cut.  Writer.roll cuts at position i only when the bytes since the last reset reach min
+// (writer.go:167-170: numChunkBytesAnnotation + len(data[offset:i+1]) < min -> continue), and
+// the count resets at every Annotate (writer.go:125-128), i.e. at every file start of a batch.
+// So the first min - 1 positions of a file are never cut points, whatever the hash says there,
+// and select_file never looks at candidates below fs + min - 1.  Per unit, skip[u] = the number
+// of leading 128-byte strip steps (8 KiB of the unit each) below the unit's first eligible
+// position; kStrip / 128 when the unit has none.  The positions the scan still covers see
+// their full 64-byte window (the halo load in front of each strip), so every candidate at an
+// eligible position is found exactly as before.  *scanned += the bytes left to scan.
+// One thread per unit; a unit spanning more than 64 files is scanned whole.
+__global__ __launch_bounds__(256) void scan_skip_kernel(
+    const uint64_t* __restrict__ offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
+    uint64_t nunits, uint32_t* __restrict__ skip, unsigned long long* __restrict__ scanned) {
+  constexpr uint64_t U = 64ull * kStrip, kStep = 64ull * 128;
+  constexpr uint32_t kAll = kStrip / 128;
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long live = 0;
+  if (u < nunits) {
+    const uint64_t ub = u * U, ue = ub + U < n ? ub + U : n;
+    uint32_t s = kAll;
+    if (ub < n) {
+      // the file holding ub: the last f < nfiles with offs[f] <= ub (offs[nfiles] = n > ub)
+      uint32_t lo = 0, hi = nfiles;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= ub) lo = mid;
+        else hi = mid;
+      }
+      uint32_t f = lo;
+      s = 0;  // a unit crowded with files is scanned whole
+      for (int k = 0; k < 64; k++, f++) {
+        if (f >= nfiles || offs[f] >= ue) {
+          s = kAll;
+          break;
+        }
+        const uint64_t ls = offs[f] + min_chunk - 1, fe = offs[f + 1];
+        if (ls < fe) {  // the file's first eligible position; later files start beyond it
+          const uint64_t first = ls > ub ? ls : ub;
+          s = first < ue ? (uint32_t)((first - ub) / kStep) : kAll;
+          break;
+        }
+      }
+      if (s < kAll && ub + s * kStep >= ue) s = kAll;
+      if (s < kAll) live = ue - (ub + s * kStep);
+    }
+    skip[u] = s;
+  }
+  // one atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
+  if ((threadIdx.x & 63) == 0 && live) atomicAdd(scanned, live);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1783,20 +1844,29 @@ hipError_t prepare_kernels() {
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
+hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
+                            uint64_t ntiles, uint32_t* skip, uint64_t* scanned, hipStream_t st) {
+  const uint64_t nunits = ntiles * kScanWaves;
+  if (nunits == 0) return hipSuccess;
+  scan_skip_kernel<<<(unsigned)((nunits + 255) / 256), 256, 0, st>>>(
+      offs, nfiles, n, min_chunk, nunits, skip, (unsigned long long*)scanned);
+  return hipGetLastError();
+}
+
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
-                       uint64_t* n_entries, uint64_t* span, hipStream_t st) {
+                       uint64_t* n_entries, uint64_t* span, hipStream_t st, const uint32_t* skip) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   if (average_bits <= 32)
     cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
                                                           mask64, ntiles, recs, unit_ctr, done_ctr,
-                                                          entries, n_entries, span);
+                                                          entries, n_entries, skip, span);
   else
     cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
                                                          mask64, ntiles, recs, unit_ctr, done_ctr,
-                                                         entries, n_entries, span);
+                                                         entries, n_entries, skip, span);
   return hipGetLastError();
 }
 

@@ -75,6 +75,8 @@ struct pfscdc_ctx {
   DevBuf<uint8_t> d_data, d_tail;
   DevBuf<TileRec> d_recs;
   DevBuf<uint32_t> d_unit_ctr;  // the scan's work-unit counter
+  DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
+  bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned)
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
@@ -119,6 +121,15 @@ const pfscdc_params& ctx_params(const pfscdc_ctx* ctx) { return ctx->params; }
 }  // namespace pfscdc
 
 namespace {
+
+// PFSCDC_SCAN_SKIP=0 scans every byte of a batch (A/B only: same results either way)
+bool scan_skip_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_SCAN_SKIP");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 
 int fail(pfscdc_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -250,6 +261,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_recs.release();
   c->d_unit_ctr.release();
   c->d_entries.release();
+  c->d_skip.release();
   c->d_counts.release();
   c->d_offs.release();
   c->d_seg_base.release();
@@ -399,10 +411,19 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
   if (c->ntiles) {  // scan + (last workgroup) compaction into the sorted entry list
+    // the first min - 1 bytes of every file hold no cut point: those strip steps are skipped
+    const uint32_t* skip = nullptr;
+    c->scan_skipped = scan_skip_enabled();
+    if (c->scan_skipped) {
+      HIP_OK(c, c->d_skip.ensure(c->ntiles * kScanWaves));
+      HIP_OK(c, launch_scan_skip(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,
+                                 c->d_skip.p, c->d_counts.p + 3, st));
+      skip = c->d_skip.p;
+    }
     const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
                           c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1,
-                          c->d_entries.p, c->d_counts.p, c->d_span.p, st));
+                          c->d_entries.p, c->d_counts.p, c->d_span.p, st, skip));
   }
   HIP_OK(c, hipEventRecord(c->ev[1], st));
   HIP_OK(c, hipEventRecord(c->ev[2], st));
@@ -531,6 +552,15 @@ uint64_t pfscdc_debug_candidates(pfscdc_ctx* c, uint64_t* out, uint64_t cap) {
       return 0;
   }
   return ne;
+}
+
+int pfscdc_last_scan_bytes(pfscdc_ctx* c, uint64_t* out) {
+  if (!c || !out) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "scan pending");
+  *out = c->nbytes;
+  if (c->scan_skipped && c->ntiles)
+    HIP_OK(c, hipMemcpy(out, c->d_counts.p + 3, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return PFSCDC_OK;
 }
 
 int pfscdc_last_timings(pfscdc_ctx* c, float out[5]) {

@@ -87,7 +87,12 @@ hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSe
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
-                       uint64_t* n_entries, uint64_t* span, hipStream_t st);
+                       uint64_t* n_entries, uint64_t* span, hipStream_t st,
+                       const uint32_t* skip = nullptr);
+// per scan work unit, the leading 128-B strip steps below its first eligible cut position
+// (file start + min - 1); *scanned += the bytes the scan still covers
+hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
+                            uint64_t ntiles, uint32_t* skip, uint64_t* scanned, hipStream_t st);
 hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
                           uint64_t* n_entries, hipStream_t st);
 hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,

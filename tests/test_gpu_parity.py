@@ -211,3 +211,38 @@ def test_hash_chain_ends_around_the_quiet_thresholds():
         a, n = int(begins[i]), int(sizes[i])
         want = hashlib.blake2b(data[a:a + n].tobytes(), digest_size=32).digest()
         assert bytes(got[i]) == want, f"range {i} ({n} B)"
+
+
+@pytest.mark.parametrize("bits,min_", [(4, 100), (6, 40_000), (10, 262_143), (12, 270_337)])
+def test_scan_skips_first_min_bytes_of_each_file(bits, min_):
+    """The scan skips the strip steps of a work unit below its first eligible position
+    (file start + min - 1: writer.go:167-170 never cuts earlier, the count resets at each
+    Annotate).  File lengths around min, around the 8 KiB step and the 256 KiB unit, empty
+    files, and a unit crowded with more than 64 small files (scanned whole); dense candidate
+    rates make hits fall right at and around every file's first eligible position."""
+    p = Ch.Params(average_bits=bits, seed=1, min=min_, max=max(4 * min_, 5000))
+    lens = [0, 1, min_ - 1, min_, min_ + 1, 0, 8191, 8192, 8193, 262_144, 262_145,
+            3 * 262_144 + 7, min_ + 8192, min_ + 8191, 2 * min_ + 262_144 + 5]
+    lens += [700] * 300                       # > 64 files inside one 256 KiB unit
+    lens += [1 << 20, (1 << 20) + 4096 * 3, 5 * min_ + 77, 0]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 1000 + bits)
+    c = chunker_for(p)
+    res = c.scan(data, offs)
+    assert_same(res, data, offs, p)
+    scanned = c.last_scan_bytes()
+    assert 0 < scanned <= int(offs[-1])
+    if min_ > 64 * 1024:
+        assert scanned < int(offs[-1]), "nothing skipped"
+
+
+def test_scan_skip_c2_layout_rolls_three_quarters():
+    # configs[1]: 4 MiB files, min 1,000,000: the first 999,999 bytes of each file hold no
+    # eligible position, 23.8% of the bytes are never rolled (whole 8 KiB steps)
+    p = DEFAULT
+    offs = np.array([i * (4 << 20) for i in range(9)], dtype=np.uint64)
+    data = synthetic_bytes(offs, 0xC2)
+    c = chunker_for(p)
+    assert_same(c.scan(data, offs), data, offs, p)
+    per_file = (4 << 20) - (999_999 // 8192) * 8192
+    assert c.last_scan_bytes() == 8 * per_file
