@@ -1188,14 +1188,14 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   uint8_t* my = s_msg + slot + 32u * j;
 
   // Absolute LDS addresses (buffer 0) of the 4 message words this lane consumes in each
-  // round, 48 registers held for the whole kernel (the buffer parity is the ds_read offset
-  // immediate).  Left to itself the compiler keeps the sigma bytes packed and rebuilds each
+  // of rounds 0-9 (10 and 11 reuse the words of 0 and 1), 40 registers held for the whole
+  // kernel (the buffer parity is the ds_read offset immediate).  Left to itself the compiler keeps the sigma bytes packed and rebuilds each
   // address with a v_add per read (48 VALU per block, ~8% of the hash); the empty asm makes
   // the values opaque so they stay in registers (budget: amdgpu_waves_per_eu(1, 2)).
   const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)s_msg;
-  uint32_t ma[12][4];
+  uint32_t ma[10][4];
 #pragma unroll
-  for (int r = 0; r < 12; r++) {
+  for (int r = 0; r < 10; r++) {
     const uint32_t pk = pick4(j, kSigmaPack[r][0], kSigmaPack[r][1], kSigmaPack[r][2], kSigmaPack[r][3]);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1277,10 +1277,18 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       x0 = lds_abs_u64(ma[0][0] + cur); x1 = lds_abs_u64(ma[0][1] + cur);
       x2 = lds_abs_u64(ma[0][2] + cur); x3 = lds_abs_u64(ma[0][3] + cur);
     }
+    // rounds 10 and 11 use sigma 0 and 1 again: their words are kept from rounds 0 and 1
+    // (16 VGPRs) instead of read from LDS a second time (8 of the block's 48 reads)
+    uint64_t sv[2][4];
 #pragma unroll
     for (int r = 0; r < 12; r++) {
+      if (r < 2) {
+        sv[r][0] = x0; sv[r][1] = x1; sv[r][2] = x2; sv[r][3] = x3;
+      }
       uint64_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
-      if (r < 11) {
+      if (r == 9 || r == 10) {
+        y0 = sv[r - 9][0]; y1 = sv[r - 9][1]; y2 = sv[r - 9][2]; y3 = sv[r - 9][3];
+      } else if (r < 11) {
         y0 = lds_abs_u64(ma[r + 1][0] + cur);
         y1 = lds_abs_u64(ma[r + 1][1] + cur);
         y2 = lds_abs_u64(ma[r + 1][2] + cur);
