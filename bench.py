@@ -104,6 +104,10 @@ def parse():
                          "affinity mask")
     ap.add_argument("--cpu-batches", type=int, default=8,
                     help="c2: configs[1] batches in the CPU-baseline sample")
+    ap.add_argument("--host-ahead", type=int, default=-1,
+                    help="one step at a time on the GPU, the host enqueuing the next step on a "
+                         "second context ordered after the current one (1/0; default: on for "
+                         "the c2 put path at one step in flight)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-chain-floor", action="store_true",
@@ -349,7 +353,14 @@ def main():
             batches.pop()
             torch.cuda.empty_cache()
     S = len(batches)
-    chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(S)]
+    # host ahead: the GPU still runs one step at a time (each step's stream waits for all of
+    # the previous step's work), but the next step is already enqueued on a second context
+    # over the same input when the current one completes, so the host-side wait, result
+    # copy and launch of a step no longer sit between two steps on the GPU
+    ahead = S == 1 and (args.host_ahead == 1 or (args.host_ahead < 0 and args.config == "c2"
+                                                 and args.path == "put"))
+    NC = 2 if ahead else S
+    chunkers = [Chunker(params, device=local, ref_ids=args.ref_ids) for _ in range(NC)]
     if S > 1 and args.hash_order == "serial":  # each hash after the previous step's hash
         for k in range(S):
             chunkers[k].order_hash_after(chunkers[(k - 1) % S])
@@ -366,7 +377,7 @@ def main():
     torch.cuda.synchronize()
     steps_t = []   # per timed step: the library's timings dict
     done_at = []   # completion times of the timed steps
-    pending = [False] * S
+    pending = [False] * NC
     last = {}
 
     def finish(k, record):
@@ -387,14 +398,16 @@ def main():
 
     def run(nsteps, record):
         for _ in range(nsteps):
-            k = seq[0] % S
+            k = seq[0] % NC
             seq[0] += 1
             if pending[k]:
                 finish(k, record)
-            chunkers[k].scan_async(batches[k], work.offs)
+            if ahead:  # after everything the other context has enqueued (the previous step)
+                chunkers[k].wait_for(chunkers[(k + 1) % NC])
+            chunkers[k].scan_async(batches[k % S], work.offs)
             pending[k] = True
-        for j in range(S):  # drain in launch order
-            kk = (seq[0] + j) % S
+        for j in range(NC):  # drain in launch order
+            kk = (seq[0] + j) % NC
             if pending[kk]:
                 finish(kk, record)
 
@@ -448,8 +461,9 @@ def main():
     roofline = roof(hash_ms, "blake2b_kernel", "blake2b_kernel") if dom_hash else \
         roof(scan_ms, "cdc_scan_kernel", "cdc_scan_kernel")
     roofline["duration_source"] = ("HIP events around the launch on the library's stream, mean "
-                                   "over the %d timed launches, %d step(s) in flight"
-                                   % (len(steps_t), S))
+                                   "over the %d timed launches, %d step(s) in flight%s"
+                                   % (len(steps_t), S, " (the host one step ahead)" if ahead
+                                      else ""))
     roofline["span_ms"] = kmean.get("hash_span" if dom_hash else "scan_span")
     if args.ref_ids and kmean.get("ref_ids", 0) > (hash_ms or 0):
         roofline = roof(kmean["ref_ids"], "blake2b_kernel<kModeRefId> (ChaCha20 + BLAKE2b of "
@@ -476,7 +490,7 @@ def main():
                                "source": tj["_source"]}
 
     info = dict(work.info)
-    info.update({"steps_in_flight": S,
+    info.update({"steps_in_flight": S, "host_ahead": ahead,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},
                  "parallelism": ("file-sharded x%d, RCCL all-gather of chunk-ref index" % world

@@ -91,6 +91,10 @@ int pfscdc_set_stream(pfscdc_ctx* ctx, void* hip_stream);
  * stream); it does not block the host.  The Python binding calls it with torch's current
  * stream before each call on a torch tensor. */
 int pfscdc_stream_wait(pfscdc_ctx* ctx, void* hip_stream);
+/* The hipStream_t the ctx enqueues on (its own, or the one given to pfscdc_set_stream), e.g.
+ * for pfscdc_stream_wait(other_ctx, pfscdc_stream_handle(ctx)): every later call of other_ctx
+ * runs after the work ctx has enqueued so far. */
+void* pfscdc_stream_handle(const pfscdc_ctx* ctx);
 
 /* Steps in flight on two ctxs of one GPU: every later scan of ctx starts its BLAKE2b kernel
  * only after the BLAKE2b kernel last enqueued by other (NULL: no ordering).  The next step's

@@ -29,6 +29,7 @@ OPT_REF_IDS = 1
 EXPORTED = [
     "pfscdc_default_params", "pfscdc_table", "pfscdc_go_int63", "pfscdc_ctx_create",
     "pfscdc_ctx_destroy", "pfscdc_last_error", "pfscdc_set_stream", "pfscdc_stream_wait",
+    "pfscdc_stream_handle",
     "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
@@ -168,6 +169,7 @@ def load() -> C.CDLL:
             "pfscdc_last_error": (C.c_char_p, [vp]),
             "pfscdc_set_stream": (i32, [vp, vp]),
             "pfscdc_stream_wait": (i32, [vp, vp]),
+            "pfscdc_stream_handle": (vp, [vp]),
             "pfscdc_order_hash_after": (i32, [vp, vp]),
             "pfscdc_scan": (i32, [vp, vp, u64, i32, P(u64), u32]),
             "pfscdc_scan_async": (i32, [vp, vp, u64, i32, P(u64), u32]),

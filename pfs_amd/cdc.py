@@ -98,6 +98,12 @@ class Chunker:
         self._check(self.lib.pfscdc_order_hash_after(self.ctx, other.ctx if other else None),
                     "order_hash_after")
 
+    def wait_for(self, other: "Chunker") -> None:
+        """Order every later call of this ctx after the work ``other`` has enqueued so far
+        (pfscdc_stream_wait on pfscdc_stream_handle(other))."""
+        h = self.lib.pfscdc_stream_handle(other.ctx)
+        self._check(self.lib.pfscdc_stream_wait(self.ctx, h), "stream_wait")
+
     def _after_torch(self, *tensors) -> None:
         """Order the ctx stream after torch's current stream (pfscdc_stream_wait) when a
         call reads or writes torch CUDA tensors, so bytes written by a torch kernel or a

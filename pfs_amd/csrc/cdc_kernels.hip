@@ -1161,6 +1161,9 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 //   BLAKE2b (the id to verify) goes to segs[].hash, and after each block's rounds the
 //   keystream is XORed into the LDS buffer and the plaintext stored to out.
 constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
+// Development trace (PFSCDC_WAVE_TRACE, timing only): per hash wave its end time and its
+// hardware slot (HW_ID, XCC_ID), to read how the launch drains.  nullptr: off.
+__device__ uint64_t* g_wave_trace = nullptr;
 template <int MODE>
 __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
@@ -1490,9 +1493,11 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // active quad at least Q blocks from its end, so pairs of fast blocks need Q >= 5
   // (one copy of the fast loop, entered after a parity-1 step: one hot loop body in the
   // instruction cache)
+  uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; the development trace)
   while (true) {
     if (!step(P0)) break;
     if (!step(P1)) break;
+    wave_steps += 2;
     if constexpr (MODE == kModeHash) {
       if (quiet >= 5) {
         uint64_t pre[4] = {lds_abs_u64(ma[0][0]), lds_abs_u64(ma[0][1]), lds_abs_u64(ma[0][2]),
@@ -1501,11 +1506,24 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
           fast_step(P0, pre);
           fast_step(P1, pre);
           quiet -= 2;
+          wave_steps += 2;
         } while (quiet >= 5);
       }
     }
   }
+  if (MODE == kModeHash && g_wave_trace && lane == 0) {
+    const uint64_t w = (uint64_t)blockIdx.x * (kHashBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // HW_REG_XCC_ID
+    g_wave_trace[4 * w] = __builtin_amdgcn_s_memrealtime();
+    g_wave_trace[4 * w + 1] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    g_wave_trace[4 * w + 2] = wave_steps;
+  }
   span_end(span);
+}
+
+hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_trace), &p, sizeof p, 0, hipMemcpyHostToDevice, st);
 }
 
 // 5d. ChaCha20 ciphertext of whole chunks, one lane per 64-byte keystream block (the Ref.Id

@@ -76,6 +76,7 @@ struct pfscdc_ctx {
   DevBuf<TileRec> d_recs;
   DevBuf<uint32_t> d_unit_ctr;  // the scan's work-unit counter
   DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
+  DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned)
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
@@ -313,6 +314,8 @@ int pfscdc_order_hash_after(pfscdc_ctx* c, pfscdc_ctx* other) {
   return PFSCDC_OK;
 }
 
+void* pfscdc_stream_handle(const pfscdc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
 int pfscdc_stream_wait(pfscdc_ctx* c, void* hip_stream) {
   if (!c) return PFSCDC_EINVAL;
   hipStream_t s = (hipStream_t)hip_stream;
@@ -438,10 +441,17 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   // enqueued hash (the scans still overlap the hash tails; two hashes never share the CUs)
   if (c->hash_after && c->hash_after->device == c->device)
     HIP_OK(c, hipStreamWaitEvent(st, c->hash_after->ev[4], 0));
+  const char* wtrace = getenv("PFSCDC_WAVE_TRACE");
+  if (wtrace) {
+    HIP_OK(c, c->d_wtrace.ensure(1 << 17));
+    HIP_OK(c, hipMemsetAsync(c->d_wtrace.p, 0, sizeof(uint64_t) << 17, st));
+    HIP_OK(c, set_wave_trace(c->d_wtrace.p, st));
+  }
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
                              c->d_span.p + 2, waves));
+  if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
@@ -493,6 +503,17 @@ int pfscdc_wait(pfscdc_ctx* c) {
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->nsegs = total;
   c->scan_valid = true;
+  if (const char* wtrace = getenv("PFSCDC_WAVE_TRACE")) {  // development trace: append
+    std::vector<uint64_t> t(1 << 17);
+    HIP_OK(c, hipMemcpy(t.data(), c->d_wtrace.p, sizeof(uint64_t) << 17, hipMemcpyDeviceToHost));
+    uint64_t sp[4];
+    HIP_OK(c, hipMemcpy(sp, c->d_span.p, sizeof sp, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(wtrace, "ab")) {
+      fwrite(sp, sizeof sp, 1, f);
+      fwrite(t.data(), sizeof(uint64_t), t.size(), f);
+      fclose(f);
+    }
+  }
   return PFSCDC_OK;
 }
 

@@ -26,7 +26,8 @@ constexpr uint32_t kStageBytes = 64u * 128u;       // per-wave LDS-DMA image: 64
 constexpr uint32_t kScanLdsBytes = kTableLdsBytes + kScanWaves * kStageBytes;
 static_assert(kScanLdsBytes <= 160 * 1024, "scan kernel LDS budget");
 constexpr int kCompactBlock = 1024;
-constexpr int kSelectBlock = 256;   // 4 files (waves) per block
+constexpr int kSelectBlock = 1024;  // 16 files (waves) per block; the last block's tail (segment
+                                    // compaction, LPT order) runs on all 1024 threads
 constexpr int kHashBlock = 256;     // 64 quads (one segment each at a time) per block
 #ifndef PFS_HASH_WAVES_PER_SIMD
 #define PFS_HASH_WAVES_PER_SIMD 2
@@ -83,6 +84,7 @@ bool ctx_scan_valid(const pfscdc_ctx* ctx);
 uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
 uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
+hipError_t set_wave_trace(uint64_t* p, hipStream_t st);  // development trace (PFSCDC_WAVE_TRACE)
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
