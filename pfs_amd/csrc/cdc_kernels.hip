@@ -597,9 +597,16 @@ PFS_DEV uint64_t block_exscan(uint64_t v, uint64_t* s_wave, uint64_t* total) {
 // separate one-workgroup launch would instead wait for a whole free CU behind the other
 // step's resident hash waves (15 ms instead of 0.2 ms with two steps in flight).
 PFS_DEV bool last_block_done(uint32_t* done_ctr, uint32_t* s_flag) {
-  __threadfence();
+  // Every wave waits until its stores have reached its XCD's L2 (vmcnt(0)); after the
+  // barrier one thread writes that L2 back and counts the workgroup done (device-scope
+  // release: a buffer_wbl2 per workgroup, not one per wave as a __threadfence in every
+  // thread would issue); the last workgroup then acquires (invalidates its L2).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
-  if (threadIdx.x == 0) *s_flag = atomicAdd(done_ctr, 1u) == gridDim.x - 1 ? 1u : 0u;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    *s_flag = atomicAdd(done_ctr, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
   __syncthreads();
   const bool last = *s_flag != 0;
   if (last) __threadfence();
@@ -763,17 +770,29 @@ PFS_DEV void select_file(
     }
     count++;
   };
-  // lower_bound(entries, fs + min - 1) on the entry value (dense markers = tile end)
+  // lower_bound(entries, fs + min - 1) on the entry value (dense markers = tile end), a
+  // 64-way search: each pass the wave's lanes test 64 evenly spaced entries and keep the
+  // stretch holding the boundary (~3 dependent loads for 10^4 entries instead of ~14)
   uint64_t k = 0;
   {
-    uint64_t lo = 0, hi = ne;
     const uint64_t key = fs + min_chunk - 1;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if ((entries[mid] & ~kDenseBit) < key) lo = mid + 1;
-      else hi = mid;
+    uint64_t lo = 0, hi = ne;  // the answer lies in [lo, hi]
+    while (hi - lo > 64) {
+      const uint64_t step = (hi - lo + 63) / 64;
+      const uint64_t i = lo + lane * step;
+      const bool below = i < hi && (entries[i] & ~kDenseBit) < key;
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(below));  // a prefix of the lanes
+      if (cnt == 0) {
+        hi = lo;
+      } else {
+        const uint64_t top = lo + (uint64_t)cnt * step;
+        lo = lo + (uint64_t)(cnt - 1) * step + 1;
+        hi = top < hi ? top : hi;
+      }
     }
-    k = lo;
+    const uint64_t i = lo + lane;
+    const bool below = i < hi && (entries[i] & ~kDenseBit) < key;
+    k = lo + (uint64_t)__popcll(__ballot(below));
   }
   uint64_t s = fs;
   while (true) {
