@@ -108,6 +108,9 @@ def parse():
                     help="one step at a time on the GPU, the host enqueuing the next step on a "
                          "second context ordered after the current one (1/0; default: on for "
                          "the c2 put path at one step in flight)")
+    ap.add_argument("--commit-hash", default="fused", choices=["fused", "separate"],
+                    help="--path commit: DataRef hashes in one launch with the chunks' content "
+                         "hashes (pfscdc_commit_refs), or the scan's own hash pass first")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-chain-floor", action="store_true",
@@ -978,6 +981,9 @@ def bench_commit(args, ctx):
     S = args.inflight if args.inflight > 0 else 1
     data = torch.empty(total, dtype=torch.uint8, device=dev)
     chunkers = [Chunker(params, device=ctx["local"]) for _ in range(S)]
+    fused = args.commit_hash == "fused"
+    for ch in chunkers:  # the DataRef hashes join the chunk content hashes (pfscdc_commit_refs)
+        ch.set_cuts_only(fused)
     fill(chunkers[0], data, work)
     poffs = work.offs
     gbyte = int(lay.offsets()[p0])  # this rank's first byte in the commit stream
@@ -997,7 +1003,11 @@ def bench_commit(args, ctx):
         coffs, hashes, known = chunker.form_chunks(streams)
         if record:
             acc["host_form_ms"] += (time.perf_counter() - h0) * 1e3
-        refs, chash = chunker.create_refs(data, coffs, hashes, known)
+        if fused:
+            refs, chash, seghash = chunker.commit_refs(data, coffs, known)
+            res.segments["hash"] = seghash
+        else:
+            refs, chash = chunker.create_refs(data, coffs, hashes, known)
         if record:
             acc["create"] += chunker.last_create_ms()
             ct = chunker.last_create_timings()
@@ -1069,6 +1079,7 @@ def bench_commit(args, ctx):
                  "filesets_this_rank": fs[1] - fs[0], "pieces_this_rank": len(work.sizes),
                  "chunks_this_rank": nch, "chunks_per_commit": int(len(chunks)),
                  "multi_dataref_chunks": int(nch - int(known.sum())),
+                 "commit_hash": args.commit_hash,
                  "steps_in_flight": S,
                  "parallelism": "fileset-sharded x%d, all-gather of the chunk records" % world
                  if world > 1 else "single GPU"})
@@ -1085,6 +1096,8 @@ def bench_commit(args, ctx):
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
         "kernel_ms": {name: round(v, 4) for name, v in avg.items()},
         "commit_chunks_digest": hashlib.blake2b(chunks.tobytes(), digest_size=16).hexdigest(),
+        "dataref_hashes_digest": hashlib.blake2b(
+            np.ascontiguousarray(last["res"].segments["hash"]).tobytes(), digest_size=16).hexdigest(),
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),

@@ -127,6 +127,10 @@ const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* ctx);
 /* Options of every following scan on ctx (bit set).  PFSCDC_OPT_REF_IDS: also compute each
  * segment's pfscdc_ref (a second BLAKE2b pass over the ChaCha20 ciphertext, fused). */
 #define PFSCDC_OPT_REF_IDS 1u
+/* PFSCDC_OPT_CUTS_ONLY: the scan finds the segments (cut positions) but leaves their DataRef
+ * hashes to a following pfscdc_commit_refs, which computes them in one launch together with
+ * the formed chunks' content hashes. */
+#define PFSCDC_OPT_CUTS_ONLY 2u
 int pfscdc_set_options(pfscdc_ctx* ctx, uint32_t options);
 /* Refs of the last completed scan, aligned with pfscdc_segments (NULL unless the scan ran
  * with PFSCDC_OPT_REF_IDS). */
@@ -160,6 +164,17 @@ int pfscdc_last_get_ms(pfscdc_ctx* ctx, float* ms);
 int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
                        const uint8_t* hash_known, pfscdc_ref* refs);
+/* The commit data plane's hashing in one pass, after a scan made with PFSCDC_OPT_CUTS_ONLY
+ * over the same bytes and pfscdc_form_chunks: every segment's DataRef hash (writer.go:301-312,
+ * into segment_hashes, 32 B each in pfscdc_segments order) and every chunk's content hash
+ * (content_hashes out; a chunk with hash_known[i] != 0 is one segment, and its hash is that
+ * segment's) run as one BLAKE2b launch in longest-first order, so the two independent sets of
+ * serial chains share the GPU instead of running one pass after the other; then
+ * chunk.Create's dek and Ref.Id as pfscdc_create_refs.  refs as pfscdc_create_refs.
+ * Synchronous; the scan's segment list is consumed (pfscdc_segments is empty afterwards). */
+int pfscdc_commit_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
+                       const uint8_t* hash_known, pfscdc_ref* refs, uint8_t* segment_hashes);
 /* hashDataRefs (fileset/util.go:149-158): FileInfo.Hash = BLAKE2b-256 over the n concatenated
  * 32-byte DataRef hashes (host array), computed by the hash kernel. */
 int pfscdc_hash_data_refs(pfscdc_ctx* ctx, const uint8_t* hashes, uint32_t n, uint8_t out[32]);

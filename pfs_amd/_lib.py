@@ -24,6 +24,7 @@ PFSCDC_ECALLBACK = -6
 SEG_VALID = 1
 SEG_CUT = 2
 OPT_REF_IDS = 1
+OPT_CUTS_ONLY = 2
 
 # Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -33,7 +34,7 @@ EXPORTED = [
     "pfscdc_scan",
     "pfscdc_scan_async", "pfscdc_wait", "pfscdc_num_segments", "pfscdc_segments",
     "pfscdc_file_segment_begin", "pfscdc_debug_candidates", "pfscdc_last_timings",
-    "pfscdc_last_scan_bytes",
+    "pfscdc_last_scan_bytes", "pfscdc_commit_refs",
     "pfscdc_set_options", "pfscdc_refs", "pfscdc_last_ref_ms", "pfscdc_get_chunks",
     "pfscdc_last_get_ms",
     "pfscdc_host_alloc", "pfscdc_host_free", "pfscdc_fill_synthetic", "pfscdc_fill_synthetic_ex", "pfscdc_writer_create",
@@ -198,6 +199,7 @@ def load() -> C.CDLL:
             "pfscdc_writer_annotation_count": (i64, [vp]),
             "pfscdc_writer_destroy": (i32, [vp]),
             "pfscdc_create_refs": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, vp]),
+            "pfscdc_commit_refs": (i32, [vp, vp, u64, i32, P(u64), u32, vp, vp, vp, vp]),
             "pfscdc_last_create_ms": (i32, [vp, P(C.c_float)]),
             "pfscdc_last_create_timings": (i32, [vp, P(C.c_float)]),
             "pfscdc_form_chunks": (i32, [vp, P(C.c_uint32), u32, P(u64), vp, vp, u64, P(u64)]),

@@ -64,14 +64,24 @@ class Chunker:
             raise _lib.PfsCdcError(rc, "pfscdc_ctx_create failed (no GPU or bad params)")
         self.ctx = ctx
         self.ref_ids = False
+        self.cuts_only = False
         if ref_ids:
             self.set_ref_ids(True)
 
+    def _set_options(self) -> None:
+        o = (_lib.OPT_REF_IDS if self.ref_ids else 0) | (_lib.OPT_CUTS_ONLY if self.cuts_only else 0)
+        self._check(self.lib.pfscdc_set_options(self.ctx, o), "set_options")
+
     def set_ref_ids(self, on: bool) -> None:
         """Also compute each segment's Ref (Id, Dek) of chunk.Create (pfscdc.h)."""
-        self._check(self.lib.pfscdc_set_options(self.ctx, _lib.OPT_REF_IDS if on else 0),
-                    "set_options")
         self.ref_ids = on
+        self._set_options()
+
+    def set_cuts_only(self, on: bool) -> None:
+        """Scans find the segments but leave their DataRef hashes to commit_refs
+        (PFSCDC_OPT_CUTS_ONLY)."""
+        self.cuts_only = on
+        self._set_options()
 
     def close(self) -> None:
         if getattr(self, "ctx", None):
@@ -234,6 +244,32 @@ class Chunker:
             self._check(rc, "form_chunks")
             k = n.value
             return offs[:k + 1].copy(), hashes[:k].copy(), known[:k].astype(bool)
+
+    def commit_refs(self, data, chunk_offsets: Sequence[int], hash_known):
+        """After a cuts-only scan of ``data`` and form_chunks: the DataRef hashes of the
+        scan's segments and the chunks' content hashes in one launch, then chunk.Create
+        (pfscdc_commit_refs).  Returns (refs REF_DTYPE[n], content_hashes uint8[n,32],
+        segment_hashes uint8[nsegs,32])."""
+        offs = _offsets_array(chunk_offsets)
+        n = len(offs) - 1
+        nsegs = int(self.lib.pfscdc_num_segments(self.ctx))
+        hashes = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        seg = np.zeros((max(nsegs, 1), 32), dtype=np.uint8)
+        known = np.ascontiguousarray(np.asarray(hash_known, dtype=np.uint8))
+        if hasattr(data, "is_cuda") and data.is_cuda:
+            ptr, nbytes, on = data.data_ptr(), data.numel(), 1
+        else:
+            arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
+                                       if isinstance(data, (bytes, bytearray)) else data,
+                                       dtype=np.uint8)
+            ptr, nbytes, on = (arr.ctypes.data if arr.size else None), arr.size, 0
+        refs = np.zeros(max(n, 1), dtype=_lib.ref_dtype())
+        rc = self.lib.pfscdc_commit_refs(self.ctx, ptr, nbytes, on,
+                                         offs.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                                         hashes.ctypes.data, known.ctypes.data if n else None,
+                                         refs.ctypes.data, seg.ctypes.data)
+        self._check(rc, "commit_refs")
+        return refs[:n], hashes[:n], seg[:nsegs]
 
     def create_refs(self, data, chunk_offsets: Sequence[int], content_hashes=None,
                     hash_known=None):

@@ -78,6 +78,7 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
   DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned)
+  bool cuts_only = false;       // the last pfscdc_scan left the DataRef hashes to commit_refs
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
@@ -334,6 +335,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                     const uint64_t* file_offsets, uint32_t nfiles, uint32_t options) {
   if (!c) return PFSCDC_EINVAL;
   if (c->pending) return fail(c, PFSCDC_ESTATE, "previous scan not waited for");
+  c->cuts_only = false;
   if (!file_offsets) return fail(c, PFSCDC_EINVAL, "file_offsets is NULL");
   if (nbytes && !bytes) return fail(c, PFSCDC_EINVAL, "bytes is NULL");
   if (file_offsets[0] != 0 || file_offsets[nfiles] != nbytes)
@@ -476,7 +478,12 @@ extern "C" {
 int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
                       const uint64_t* file_offsets, uint32_t nfiles) {
   if (!c) return PFSCDC_EINVAL;
-  return scan_async_impl(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles, c->options);
+  const uint32_t o = c->options;
+  const bool cuts = (o & PFSCDC_OPT_CUTS_ONLY) != 0;
+  const int rc = scan_async_impl(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles,
+                                 (o & ~PFSCDC_OPT_CUTS_ONLY) | (cuts ? kScanNoHash : 0u));
+  if (rc == PFSCDC_OK) c->cuts_only = cuts;
+  return rc;
 }
 
 int pfscdc_wait(pfscdc_ctx* c) {
@@ -542,7 +549,7 @@ int pfscdc_scan(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_
 uint64_t pfscdc_num_segments(const pfscdc_ctx* c) { return c ? c->nsegs : 0; }
 
 int pfscdc_set_options(pfscdc_ctx* c, uint32_t options) {
-  if (!c || (options & ~PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
+  if (!c || (options & ~(PFSCDC_OPT_REF_IDS | PFSCDC_OPT_CUTS_ONLY))) return PFSCDC_EINVAL;
   if (c->pending) return fail(c, PFSCDC_ESTATE, "set_options during a pending scan");
   c->options = options;
   return PFSCDC_OK;
@@ -704,6 +711,113 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
   }
   return create_refs_device(c, data, nbytes, chunk_offsets, nchunks, content_hashes, hash_known,
                             refs);
+}
+
+int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
+                       const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
+                       const uint8_t* hash_known, pfscdc_ref* refs, uint8_t* segment_hashes) {
+  if (!c) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "commit_refs during a pending scan");
+  if (!c->scan_valid || !c->cuts_only || !c->dev_data)
+    return fail(c, PFSCDC_ESTATE, "commit_refs needs the last scan made with PFSCDC_OPT_CUTS_ONLY");
+  if (!chunk_offsets || (nchunks && (!refs || !content_hashes || !hash_known)) ||
+      (c->nsegs && !segment_hashes))
+    return fail(c, PFSCDC_EINVAL, "NULL argument");
+  if (nbytes != c->nbytes || (bytes_on_device && (const uint8_t*)bytes != c->dev_data))
+    return fail(c, PFSCDC_EINVAL, "commit_refs must get the bytes of the last scan");
+  if (chunk_offsets[0] != 0 || chunk_offsets[nchunks] != nbytes)
+    return fail(c, PFSCDC_EINVAL, "chunk_offsets must start at 0 and end at nbytes");
+  for (uint32_t i = 0; i < nchunks; i++)
+    if (chunk_offsets[i + 1] < chunk_offsets[i])
+      return fail(c, PFSCDC_EINVAL, "chunk_offsets must be nondecreasing");
+  HIP_OK(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const uint8_t* data = c->dev_data;  // the scan's device copy (or the caller's device bytes)
+  // the scan's segments as absolute ranges (the ctx buffers are reused below)
+  const uint64_t m = c->nsegs;
+  std::vector<uint64_t> sbeg(m), ssz(m);
+  for (uint64_t s = 0; s < m; s++) {
+    const pfscdc_segment& g = c->h_segs.p[s];
+    sbeg[s] = c->h_offs.p[g.file] + g.offset;
+    ssz[s] = g.size;
+  }
+  // one record list: the chunks whose content hash is unknown, then every segment; all
+  // absolute (file 0, offs = {0}), hashed in one LPT-ordered launch
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < nchunks; i++) k += hash_known[i] ? 0 : 1;
+  const uint64_t R = k + m;
+  if (R > 0xffffffffull) return fail(c, PFSCDC_EUNSUPPORTED, "too many records");
+  HIP_OK(c, c->h_segs.ensure(R ? R : 1));
+  HIP_OK(c, c->h_offs.ensure(1));
+  c->h_offs.p[0] = 0;
+  uint64_t longest = 0, sum = 0;
+  {
+    uint64_t r = 0;
+    auto put = [&](uint64_t start, uint64_t size, uint32_t tag) {
+      pfscdc_segment& g = c->h_segs.p[r++];
+      std::memset(&g, 0, sizeof g);
+      g.offset = start;
+      g.size = size;
+      g.file = 0;
+      g.flags = PFSCDC_SEG_VALID;
+      (void)tag;
+      longest = std::max(longest, size);
+      sum += size;
+    };
+    for (uint32_t i = 0; i < nchunks; i++)
+      if (!hash_known[i]) put(chunk_offsets[i], chunk_offsets[i + 1] - chunk_offsets[i], i);
+    for (uint64_t s = 0; s < m; s++) put(sbeg[s], ssz[s], 0);
+  }
+  HIP_OK(c, c->d_offs.ensure(1));
+  HIP_OK(c, c->d_segs.ensure(R ? R : 1));
+  HIP_OK(c, c->d_order.ensure(R ? R : 1));
+  HIP_OK(c, c->d_qctr.ensure(2));
+  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->h_seg_begin.ensure(1));
+  c->h_seg_begin.p[0] = R;
+  HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  if (R)
+    HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * R,
+                             hipMemcpyHostToDevice, st));
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+  hipEvent_t e0 = c->ev[0], e1 = c->ev[1];
+  HIP_OK(c, hipEventRecord(e0, st));
+  if (R)
+    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, R, c->d_order.p,
+                             c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
+                             hash_waves(longest, sum, c->num_cus)));
+  HIP_OK(c, hipEventRecord(e1, st));
+  if (R)
+    HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * R,
+                             hipMemcpyDeviceToHost, st));
+  HIP_OK(c, hipStreamSynchronize(st));
+  float pass_ms = 0.f;
+  HIP_OK(c, hipEventElapsedTime(&pass_ms, e0, e1));
+  for (uint64_t s = 0; s < m; s++) std::memcpy(segment_hashes + 32 * s, c->h_segs.p[k + s].hash, 32);
+  // content hashes: computed, or (one-segment chunks) the segment's, matched by range
+  {
+    uint32_t r = 0;
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < nchunks; i++) {
+      const uint64_t a = chunk_offsets[i], z = chunk_offsets[i + 1] - a;
+      if (!hash_known[i]) {
+        std::memcpy(content_hashes + 32ull * i, c->h_segs.p[r++].hash, 32);
+        continue;
+      }
+      while (s < m && (sbeg[s] < a || (sbeg[s] == a && ssz[s] != z))) s++;
+      if (s == m) return fail(c, PFSCDC_EINVAL, "a one-segment chunk matches no segment");
+      std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * s, 32);
+    }
+  }
+  c->scan_valid = false;
+  c->nsegs = 0;
+  std::vector<uint8_t> all(nchunks, 1);
+  const int rc = create_refs_device(c, data, nbytes, chunk_offsets, nchunks, content_hashes,
+                                    all.data(), refs);
+  c->create_hash_ms = pass_ms;  // the union pass (DataRef + content hashes)
+  c->create_ms += pass_ms;
+  return rc;
 }
 
 int pfscdc_hash_data_refs(pfscdc_ctx* c, const uint8_t* hashes, uint32_t n, uint8_t out[32]) {

@@ -1,0 +1,84 @@
+"""GPU parity of pfscdc_commit_refs, the commit data plane's hashing in one pass: a
+cuts-only scan (PFSCDC_OPT_CUTS_ONLY), pfscdc_form_chunks, then one BLAKE2b launch over every
+segment (DataRef.Hash, writer.go:301-312) and every multi-DataRef chunk (chunk content hash,
+writer.go:233-253) followed by chunk.Create (transform.go:26-46,173-188).  Bar: bit-identical
+to the separate passes (scan with segment hashes, pfscdc_create_refs), which the other GPU
+suites check against the oracle, and to the oracle directly on a sample."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import chunker as Ch
+from pfs_amd.cdc import ChunkParams, Chunker, synthetic_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def both_ways(p: Ch.Params, offs, streams, data):
+    cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+    a = Chunker(cp, 0)
+    ra = a.scan(data, offs)
+    coffs, hashes, known = a.form_chunks(streams)
+    refs_a, chash_a = a.create_refs(data, coffs, hashes, known)
+    b = Chunker(cp, 0)
+    b.set_cuts_only(True)
+    rb = b.scan(data, offs)
+    for f in ("offset", "size", "file", "flags"):
+        assert np.array_equal(rb.segments[f], ra.segments[f]), f"segment {f} differs" 
+    coffs_b, _, known_b = b.form_chunks(streams)
+    assert np.array_equal(coffs_b, coffs) and np.array_equal(known_b, known)
+    refs_b, chash_b, seg_b = b.commit_refs(data, coffs_b, known_b)
+    assert np.array_equal(seg_b, ra.segments["hash"]), "DataRef hashes differ"
+    assert np.array_equal(chash_b, chash_a), "chunk content hashes differ"
+    assert np.array_equal(refs_b["id"], refs_a["id"]) and np.array_equal(refs_b["dek"], refs_a["dek"])
+    a.close()
+    b.close()
+    return coffs, known, refs_b, chash_b, ra
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_commit_refs_equal_separate_passes_small_params(seed):
+    # many multi-DataRef chunks: small files under a 4 KiB .. 60 KB chunker, three streams
+    p = Ch.Params(average_bits=13, seed=1, min=4000, max=60000)
+    rng = np.random.default_rng(seed)
+    lens = np.concatenate([rng.integers(0, 9000, 300), [0, 1, 3999, 4000, 60000, 60001],
+                           rng.integers(20_000, 200_000, 40)])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 300 + seed)
+    nf = len(lens)
+    streams = [0, nf // 3, nf // 3, 2 * nf // 3, nf]  # an empty stream too
+    coffs, known, refs, chash, _ = both_ways(p, offs, streams, data)
+    assert (~known.astype(bool)).sum() > 20
+    for i in np.linspace(0, len(coffs) - 2, 12).astype(int):
+        chunk = data[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        assert bytes(chash[i]) == hashlib.blake2b(chunk, digest_size=32).digest()
+        rid, dek = Ch.create_ref_id(chunk)
+        assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek
+
+
+def test_commit_refs_default_params_device_resident():
+    import torch
+
+    p = Ch.Params()
+    lens = [3 << 20, 12345, (9 << 20) + 7, 999_999, 1_000_000, 0, (21 << 20) + 5, 4 << 20]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    c = Chunker(ChunkParams(), 0)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c.fill_synthetic(t, offs, 0xC4)
+    both_ways(p, offs, [0, 3, len(lens)], t)
+    c.close()
+
+
+def test_commit_refs_needs_a_cuts_only_scan():
+    from pfs_amd import _lib
+
+    p = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+    offs = np.array([0, 50_000, 90_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 5)
+    c = Chunker(ChunkParams(p.average_bits, p.seed, p.min, p.max), 0)
+    c.scan(data, offs)
+    coffs, _, known = c.form_chunks()
+    with pytest.raises(_lib.PfsCdcError):
+        c.commit_refs(data, coffs, known)
+    c.close()
