@@ -1996,7 +1996,7 @@ static unsigned hash_grid(uint64_t max_segments, int num_cus, int waves) {
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
-                          bool ordered, uint64_t* span, int waves) {
+                          bool ordered, uint64_t* span, int waves, uint32_t prio) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   if (kHashLanesPerSegment == 1) {
@@ -2009,8 +2009,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
     return hipGetLastError();
   }
   blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
-      data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr, hash_prio_blocks(),
-      span);
+      data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
+      prio ? prio : hash_prio_blocks(), span);
   return hipGetLastError();
 }
 

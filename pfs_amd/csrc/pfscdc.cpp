@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -102,6 +103,8 @@ struct pfscdc_ctx {
   float create_ms = 0.f, create_hash_ms = 0.f;
   hipEvent_t cev = nullptr;  // create_refs: between the content-hash and the Ref.Id passes
   hipEvent_t wev = nullptr;  // pfscdc_stream_wait: the caller's stream position
+  hipStream_t aux_stream = nullptr;      // create_refs: the second Ref.Id stream (lazy)
+  hipEvent_t xev[2] = {nullptr, nullptr};  // its fork / join events
   std::vector<uint32_t> perm;  // create_refs: record -> chunk
   bool have_refs = false;
   bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
@@ -297,6 +300,9 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   if (c->cev) (void)hipEventDestroy(c->cev);
   if (c->wev) (void)hipEventDestroy(c->wev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+  for (auto& e : c->xev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return PFSCDC_OK;
 }
@@ -1129,6 +1135,25 @@ int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
 // Split Ref.Id pass (ChaCha20 in parallel, then BLAKE2b of the ciphertext) when the chunk list
 // cannot fill the hash grid's quads, i.e. the pass is bound by its longest chains.
 // PFSCDC_REFID_SPLIT=0/1 forces either form (A/B and tests).
+static bool refid_twostream() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_REFID_TWOSTREAM");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// the long subset of a two-stream Ref.Id pass: chunks longer than this percentage of the
+// longest (PFSCDC_REFID_LONG_PCT, A/B; default 65)
+static uint64_t refid_long_pct() {
+  static const uint64_t v = [] {
+    const char* e = getenv("PFSCDC_REFID_LONG_PCT");
+    const int x = e ? atoi(e) : 0;
+    return (uint64_t)(x > 0 && x < 100 ? x : 65);
+  }();
+  return v;
+}
+
 static bool refid_split(uint32_t n, int num_cus) {
   const char* e = getenv("PFSCDC_REFID_SPLIT");
   if (e && *e) return atoi(e) != 0;
@@ -1156,6 +1181,27 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
     if (!(known && known[i])) c->perm[k++] = i;
   for (uint32_t i = 0, r = k; i < n; i++)
     if (known && known[i]) c->perm[r++] = i;
+  // With every content hash known (pfscdc_commit_refs), a split Ref.Id pass runs on two
+  // streams: the chunks longer than half the longest first on the ctx stream (their ChaCha20
+  // pass is short, so the serial BLAKE2b chains that bound the pass start right away), the
+  // rest on a second stream beside them (its ChaCha20 pass and shorter chains fit in the long
+  // chains' shadow).  PFSCDC_REFID_TWOSTREAM=0: one stream (A/B).
+  // The split point: the long set is the chunks longer than 65% of the longest
+  // (PFSCDC_REFID_LONG_PCT, A/B).  c4 commit, Ref.Id pass: 50% 230, 65% 208-211, 80% 227,
+  // 90% 246 ms, one stream 240 ms: a larger long set lengthens its own ChaCha20 pass, a
+  // smaller one leaves rest chains that outlast the longest one (they run at two waves per
+  // SIMD, slower than a lone chain).
+  uint32_t nl = 0;
+  if (k == 0 && n > 1 && refid_twostream()) {
+    std::vector<uint64_t> z(n);
+    uint64_t longest = 0;
+    for (uint32_t i = 0; i < n; i++) longest = std::max(longest, z[i] = offs[i + 1] - offs[i]);
+    const uint64_t thr = longest * refid_long_pct() / 100;
+    auto is_long = [&](uint32_t i) { return z[i] > thr; };
+    std::stable_partition(c->perm.begin(), c->perm.end(), is_long);
+    for (uint32_t i = 0; i < n; i++) nl += is_long(i) ? 1 : 0;
+    if (nl == n) nl = 0;
+  }
   HIP_OK(c, c->h_offs.ensure(n + 1));
   std::memcpy(c->h_offs.p, offs, sizeof(uint64_t) * (n + 1));
   HIP_OK(c, c->h_segs.ensure(n));
@@ -1172,17 +1218,19 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   HIP_OK(c, c->d_segs.ensure(n));
   HIP_OK(c, c->d_refs.ensure(n));
   HIP_OK(c, c->d_order.ensure(n));
-  HIP_OK(c, c->d_qctr.ensure(2));
-  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->d_qctr.ensure(3));
+  HIP_OK(c, c->d_counts.ensure(6));
   HIP_OK(c, c->h_refs.ensure(n));
-  HIP_OK(c, c->h_seg_begin.ensure(2));
-  c->h_seg_begin.p[0] = k;  // pinned sources of the two device record counts
+  HIP_OK(c, c->h_seg_begin.ensure(4));
+  c->h_seg_begin.p[0] = k;  // pinned sources of the device record counts
   c->h_seg_begin.p[1] = n;
+  c->h_seg_begin.p[2] = nl;
+  c->h_seg_begin.p[3] = n - nl;
   HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (n + 1),
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * n,
                            hipMemcpyHostToDevice, st));
-  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, 2 * sizeof(uint64_t),
+  HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, 4 * sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
   uint64_t longest_k = 0, sum_k = 0, longest_n = 0, sum_n = 0;
   for (uint32_t r = 0; r < n; r++) {
@@ -1220,22 +1268,70 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
       split = false;
   }
   if (split) {
-    HIP_OK(c, c->h_blk.ensure(n + 1));
-    HIP_OK(c, c->d_blk.ensure(n + 1));
+    // 64-B block prefix per record subset: [0, nl) from h_blk[0], [nl, n) from h_blk[nl + 1]
+    HIP_OK(c, c->h_blk.ensure(n + 2));
+    HIP_OK(c, c->d_blk.ensure(n + 2));
     HIP_OK(c, c->d_segs2.ensure(n));
     HIP_OK(c, c->h_segs2.ensure(n));
+    uint64_t longest_a = 0, sum_a = 0, longest_b = 0, sum_b = 0;
     c->h_blk.p[0] = 0;
-    for (uint32_t r = 0; r < n; r++) c->h_blk.p[r + 1] = c->h_blk.p[r] + (c->h_segs.p[r].size + 63) / 64;
-    HIP_OK(c, hipMemcpyAsync(c->d_blk.p, c->h_blk.p, sizeof(uint64_t) * (n + 1),
+    for (uint32_t r = 0; r < nl; r++) {
+      const uint64_t z = c->h_segs.p[r].size;
+      c->h_blk.p[r + 1] = c->h_blk.p[r] + (z + 63) / 64;
+      longest_a = std::max(longest_a, z);
+      sum_a += z;
+    }
+    c->h_blk.p[nl + 1] = 0;
+    for (uint32_t r = nl; r < n; r++) {
+      const uint64_t z = c->h_segs.p[r].size;
+      c->h_blk.p[r + 2] = c->h_blk.p[r + 1] + (z + 63) / 64;
+      longest_b = std::max(longest_b, z);
+      sum_b += z;
+    }
+    HIP_OK(c, hipMemcpyAsync(c->d_blk.p, c->h_blk.p, sizeof(uint64_t) * (n + 2),
                              hipMemcpyHostToDevice, st));
     HIP_OK(c, launch_deks(c->d_segs.p, c->d_counts.p + 2, n, c->d_refs.p, c->d_qctr.p + 1, st));
-    HIP_OK(c, launch_chacha_xor(data, c->d_offs.p, c->d_segs.p, c->d_blk.p, n, c->h_blk.p[n],
-                                c->d_refs.p, ct, c->num_cus, st));
-    HIP_OK(c, hipMemcpyAsync(c->d_segs2.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
-                             hipMemcpyDeviceToDevice, st));
-    HIP_OK(c, launch_blake2b(ct, c->d_offs.p, c->d_segs2.p, c->d_counts.p + 2, n, c->d_order.p,
-                             c->d_qctr.p + 1, c->num_cus, nbytes, st, false, nullptr,
-                             hash_waves(longest_n, sum_n, c->num_cus)));
+    // subset [r0, r0 + m) on stream s: ChaCha20 into ct, then BLAKE2b of the ciphertext
+    // (pb: where the subset's block prefix starts in h_blk / d_blk)
+    auto chacha_pass = [&](uint32_t r0, uint32_t m, uint32_t pb, hipStream_t s) {
+      return launch_chacha_xor(data, c->d_offs.p, c->d_segs.p + r0, c->d_blk.p + pb, m,
+                               c->h_blk.p[pb + m], c->d_refs.p + r0, ct, c->num_cus, s);
+    };
+    auto refid_pass = [&](uint32_t r0, uint32_t m, uint32_t pb, const uint64_t* d_count,
+                          uint32_t* ctr, uint64_t longest, uint64_t sum, hipStream_t s,
+                          uint32_t prio, bool chacha) -> hipError_t {
+      hipError_t e = chacha ? chacha_pass(r0, m, pb, s) : hipSuccess;
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c->d_segs2.p + r0, c->d_segs.p + r0, sizeof(pfscdc_segment) * m,
+                           hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess)
+        e = launch_blake2b(ct, c->d_offs.p, c->d_segs2.p + r0, d_count, m, c->d_order.p + r0,
+                           ctr, c->num_cus, nbytes, s, false, nullptr,
+                           hash_waves(longest, sum, c->num_cus), prio);
+      return e;
+    };
+    if (nl) {
+      if (!c->aux_stream) {
+        HIP_OK(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        for (auto& e : c->xev) HIP_OK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+      // the long chunks' ChaCha20 pass has the GPU to itself; then their BLAKE2b chains start
+      // while the rest's ChaCha20 pass and chains run beside them on the second stream, the
+      // long chains' waves issuing first on every SIMD they share (s_setprio 2 while a quad
+      // has more than one block left)
+      HIP_OK(c, chacha_pass(0, nl, 0, st));
+      HIP_OK(c, hipEventRecord(c->xev[0], st));
+      HIP_OK(c, hipStreamWaitEvent(c->aux_stream, c->xev[0], 0));
+      HIP_OK(c, refid_pass(0, nl, 0, c->d_counts.p + 3, c->d_qctr.p + 1, longest_a, sum_a, st,
+                           1u, false));
+      HIP_OK(c, refid_pass(nl, n - nl, nl + 1, c->d_counts.p + 4, c->d_qctr.p + 2, longest_b,
+                           sum_b, c->aux_stream, 0u, true));
+      HIP_OK(c, hipEventRecord(c->xev[1], c->aux_stream));
+      HIP_OK(c, hipStreamWaitEvent(st, c->xev[1], 0));
+    } else {
+      HIP_OK(c, refid_pass(0, n, 1, c->d_counts.p + 2, c->d_qctr.p + 1, longest_n, sum_n, st,
+                           0u, true));
+    }
   } else {
     HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
