@@ -1429,11 +1429,15 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       const uint64_t rem64 = active ? nblk - blk : 0;
       const uint32_t rem = rem64 > 0xffffffffULL ? 0xffffffffu : (uint32_t)rem64;
       uint32_t q = wave_min_u32(active ? rem : 0xffffffffu) - 1;
-      if ((prio_blocks & 0x3fffffffu) && !graded) {
+      if (prio_blocks & 0x3fffffffu) {
+        // the next block at which the longest chain left crosses a priority threshold
         const uint32_t T = prio_blocks & 0x3fffffffu, rmax = wave_max_u32(rem);
-        if (rmax > T && rmax - T - 1 < q) q = rmax - T - 1;
+        const uint32_t th[3] = {graded ? 2 * T : T, T, T / 2};
+#pragma unroll
+        for (int i = 0; i < (graded ? 3 : 1); i++)
+          if (rmax > th[i] && rmax - th[i] - 1 < q) q = rmax - th[i] - 1;
       }
-      quiet = graded ? 0u : q;
+      quiet = q;
     }
     const bool last = !fast && blk + 1 == nblk;
     if (MODE == kModeRefId) {
