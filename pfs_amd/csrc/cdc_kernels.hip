@@ -1546,7 +1546,11 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
 }
 
 hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {
-  return hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_trace), &p, sizeof p, 0, hipMemcpyHostToDevice, st);
+  // stream-ordered and synchronous w.r.t. the host value (a development tool: the copy
+  // source must outlive the call)
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_trace), &p, sizeof p, 0, hipMemcpyHostToDevice);
 }
 
 // 5d. ChaCha20 ciphertext of whole chunks, one lane per 64-byte keystream block (the Ref.Id

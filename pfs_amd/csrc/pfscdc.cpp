@@ -787,7 +787,7 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
                              hipMemcpyHostToDevice, st));
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
-  hipEvent_t e0 = c->ev[0], e1 = c->ev[1];
+  hipEvent_t e0 = c->ev[7], e1 = c->cev;  // create_refs_device records them again below
   HIP_OK(c, hipEventRecord(e0, st));
   if (R)
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, R, c->d_order.p,
