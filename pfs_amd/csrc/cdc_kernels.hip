@@ -2004,7 +2004,8 @@ static unsigned hash_grid(uint64_t max_segments, int num_cus, int waves) {
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
-                          bool ordered, uint64_t* span, int waves, uint32_t prio) {
+                          bool ordered, uint64_t* span, int waves, uint32_t prio,
+                          bool cu_exclusive) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   if (kHashLanesPerSegment == 1) {
@@ -2016,7 +2017,13 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                                                                    order, counter, nbytes);
     return hipGetLastError();
   }
-  blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
+  // cu_exclusive: 64 KiB of unused dynamic LDS on top of the 20 KiB message buffers, so no
+  // two workgroups (of this or of another launch) share a CU.  A chain-bound launch at one
+  // wave per SIMD has one workgroup per CU anyway; the reservation keeps a second such launch
+  // in flight (configs[2]'s two streams) off its CUs, where the two launches' chains would
+  // share SIMDs (hash 215 instead of 180 ms when the dispatcher put them together).
+  const size_t dyn = cu_exclusive ? 64u * 1024u : 0u;
+  blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, dyn, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
       prio ? prio : hash_prio_blocks(), span);
   return hipGetLastError();

@@ -127,6 +127,15 @@ const pfscdc_params& ctx_params(const pfscdc_ctx* ctx) { return ctx->params; }
 
 namespace {
 
+// PFSCDC_HASH_CU_EXCLUSIVE=0: chain-bound scan hashes may share CUs with another launch (A/B)
+bool hash_cu_exclusive() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_HASH_CU_EXCLUSIVE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // PFSCDC_SCAN_SKIP=0 scans every byte of a batch (A/B only: same results either way)
 bool scan_skip_enabled() {
   static const bool on = [] {
@@ -458,7 +467,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
-                             c->d_span.p + 2, waves));
+                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive()));
   if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);

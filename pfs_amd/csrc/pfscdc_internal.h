@@ -111,7 +111,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered = false, uint64_t* span = nullptr, int waves = 0,
-                          uint32_t prio = 0);  // prio: issue-priority threshold (0: default)
+                          uint32_t prio = 0,  // prio: issue-priority threshold (0: default)
+                          bool cu_exclusive = false);  // one workgroup per CU (see launcher)
 // waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all
 int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
