@@ -1095,8 +1095,10 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 // b ^ c in the 2-cycle plain v_xor_b32 form: 16 four-cycle + 6 two-cycle ops per G instead
 // of 18 + 4 (issue-rate table).
 // Hazards: a DPP read needs 2 wait states after the VALU write of its source; the DPP sources
-// here (a, c, d) were last written 6+ instructions earlier, and each round starts with
-// s_nop 1 for whatever the compiler placed before it.
+// here (a, c, d) were last written 6+ instructions earlier, inside the previous round's asm
+// (the first G of a block has no DPP operand).  No s_nop guards the compiler's code between
+// rounds (it writes none of v100-v107 there): tests/test_dpp_hazards.py checks every DPP
+// instruction of the compiled library (an s_nop 1 per round cost 2% of a lone chain).
 #define PFS_DPP(P) " quad_perm:" P " row_mask:0xf bank_mask:0xf\n"
 #define PFS_G_ASM(PA, PC, PD, XL, XH, Y)                               \
   "v_add_co_u32_dpp v100, vcc, v100, " XL PFS_DPP(PA)                  \
@@ -1161,10 +1163,10 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 #define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                                  \
   do {                                                                                        \
     if (FIRST)                                                                                \
-      asm volatile("s_nop 1\n" PFS_G_ASM_PLAIN("%[x0]", "%[x1]") PFS_DIAG_G                    \
+      asm volatile(PFS_G_ASM_PLAIN("%[x0]", "%[x1]") PFS_DIAG_G                    \
                  PFS_ROUND_OPS(x0_, x1_, x2_, x3_));                                          \
     else                                                                                      \
-      asm volatile("s_nop 1\n" PFS_G_ASM(PFS_QP_R1, PFS_QP_R3, PFS_QP_R2, "%[x0l]", "%[x0h]", \
+      asm volatile(PFS_G_ASM(PFS_QP_R1, PFS_QP_R3, PFS_QP_R2, "%[x0l]", "%[x0h]", \
                                          "%[x1]") PFS_DIAG_G                                   \
                  PFS_ROUND_OPS(x0_, x1_, x2_, x3_));                                          \
   } while (0)
