@@ -1351,9 +1351,13 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // A block in a run of quiet blocks (content hash only): every active quad is at least 4
   // blocks from its end, so nothing in it depends on a lane's position in its chain.  Runs
   // of these execute in their own loop, straight-line code between the round blocks.
+  // the fast loop's byte counter t (lane 0 only: ((blk + 1) << 7) & t_mask), advanced by one
+  // 64-bit add per block instead of rebuilt from blk (shift, add, two selects)
+  uint64_t tm = 0;
+  const uint64_t tinc = 128 & t_mask;
   auto fast_step = [&](auto par, uint64_t* pre) {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
-    uint64_t a = ha, b = hb, c = iv_c, d = iv_d ^ (((blk + 1) << 7) & t_mask);
+    uint64_t a = ha, b = hb, c = iv_c, d = iv_d ^ tm;
     rounds(par, a, b, c, d, [&] {
       if (active) {
         lds_put(nxt);
@@ -1362,6 +1366,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     }, pre);
     ha ^= a ^ c;
     hb ^= b ^ d;
+    tm += tinc;
     blk++;  // inactive quads too: a refill resets blk
   };
 
@@ -1527,6 +1532,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       if (quiet >= 5) {
         uint64_t pre[4] = {lds_abs_u64(ma[0][0]), lds_abs_u64(ma[0][1]), lds_abs_u64(ma[0][2]),
                            lds_abs_u64(ma[0][3])};  // buffer 0 (P0): the next block
+        tm = ((blk + 1) << 7) & t_mask;
         do {
           fast_step(P0, pre);
           fast_step(P1, pre);
