@@ -1181,6 +1181,29 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
 // MODE kModeGet:   chunk.Get (transform.go:50-78): the segments are stored chunks; their
 //   BLAKE2b (the id to verify) goes to segs[].hash, and after each block's rounds the
 //   keystream is XORed into the LDS buffer and the plaintext stored to out.
+// The feed-forward h ^= v[0..7] ^ v[8..15] straight from the diagonal layout the last round
+// leaves (a, c, d rotated as DPP operands of the XORs, 8 VALU instead of 6 DPP moves back to
+// the column layout and 4 three-way XORs).  a, c, d were last written inside the round's asm,
+// 5+ instructions earlier (checked with the rest by tests/test_dpp_hazards.py).
+PFS_DEV void fold_diag(uint64_t& ha, uint64_t& hb, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  uint32_t hal = (uint32_t)ha, hah = (uint32_t)(ha >> 32), hbl = (uint32_t)hb,
+           hbh = (uint32_t)(hb >> 32);
+  asm volatile(
+      "v_xor_b32_dpp %0, %4, %0 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %1, %5, %1 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %0, %6, %0 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %1, %7, %1 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32 %2, %8, %2\n"
+      "v_xor_b32 %3, %9, %3\n"
+      "v_xor_b32_dpp %2, %10, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %3, %11, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      : "+v"(hal), "+v"(hah), "+v"(hbl), "+v"(hbh)
+      : "v"((uint32_t)a), "v"((uint32_t)(a >> 32)), "v"((uint32_t)c), "v"((uint32_t)(c >> 32)),
+        "v"((uint32_t)b), "v"((uint32_t)(b >> 32)), "v"((uint32_t)d), "v"((uint32_t)(d >> 32)));
+  ha = ((uint64_t)hah << 32) | hal;
+  hb = ((uint64_t)hbh << 32) | hbl;
+}
+
 constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
 // Development trace (PFSCDC_WAVE_TRACE, timing only): per hash wave its end time and its
 // hardware slot (HW_ID, XCC_ID), to read how the launch drains.  nullptr: off.
@@ -1289,7 +1312,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // pre (optional): round 0's message words, already read (the quiet-run loop reads the next
   // block's at round 11 into pre, from the buffer round 5 staged it in).
   auto rounds = [&](auto par, uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
-                    auto&& put_next, uint64_t* pre = nullptr) {
+                    auto&& put_next, uint64_t* pre = nullptr, bool back = true) {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1342,9 +1365,11 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       if (r == 5) put_next();
     }
 #ifndef PFS_HASH_CXX
-    a = quad_perm64<0x39>(a);  // back to the column layout
-    c = quad_perm64<0x93>(c);
-    d = quad_perm64<0x4E>(d);
+    if (back) {
+      a = quad_perm64<0x39>(a);  // back to the column layout
+      c = quad_perm64<0x93>(c);
+      d = quad_perm64<0x4E>(d);
+    }
 #endif
   };
 
@@ -1363,9 +1388,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         lds_put(nxt);
         msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
       }
-    }, pre);
-    ha ^= a ^ c;
-    hb ^= b ^ d;
+    }, pre, false);
+    fold_diag(ha, hb, a, b, c, d);
     tm += tinc;
     blk++;  // inactive quads too: a refill resets blk
   };
