@@ -540,6 +540,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   std::string errmsg;  // pfscdc_uw_last_error
 
   int fail(int rc, const char* what = nullptr) {
+    join();  // the background group write uses the data ctx (and its error string) too
     if (!err) {
       err = rc;
       errmsg = std::string(what ? what : "unordered writer") + " failed (status " +

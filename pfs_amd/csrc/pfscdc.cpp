@@ -79,6 +79,7 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
   DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned)
+  uint64_t scanned_bytes = 0;   // bytes the last waited-for scan rolled (copied in pfscdc_wait)
   bool cuts_only = false;       // the last pfscdc_scan left the DataRef hashes to commit_refs
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
@@ -402,7 +403,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
   HIP_OK(c, c->d_span.ensure(4));
-  HIP_OK(c, c->h_span.ensure(4));
+  HIP_OK(c, c->h_span.ensure(5));
 
   const uint8_t* data;
   if (bytes_on_device) {
@@ -521,8 +522,14 @@ int pfscdc_wait(pfscdc_ctx* c) {
   }
   HIP_OK(c, hipMemcpyAsync(c->h_span.p, c->d_span.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c->stream));
+  // the rolled-byte count now: later calls on this ctx reuse d_counts
+  const bool skipped = c->scan_skipped && c->ntiles;
+  if (skipped)
+    HIP_OK(c, hipMemcpyAsync(c->h_span.p + 4, c->d_counts.p + 3, sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->scanned_bytes = skipped ? c->h_span.p[4] : c->nbytes;
   c->nsegs = total;
   c->scan_valid = true;
   if (const char* wtrace = getenv("PFSCDC_WAVE_TRACE")) {  // development trace: append
@@ -600,9 +607,7 @@ uint64_t pfscdc_debug_candidates(pfscdc_ctx* c, uint64_t* out, uint64_t cap) {
 int pfscdc_last_scan_bytes(pfscdc_ctx* c, uint64_t* out) {
   if (!c || !out) return PFSCDC_EINVAL;
   if (c->pending) return fail(c, PFSCDC_ESTATE, "scan pending");
-  *out = c->nbytes;
-  if (c->scan_skipped && c->ntiles)
-    HIP_OK(c, hipMemcpy(out, c->d_counts.p + 3, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  *out = c->scanned_bytes;
   return PFSCDC_OK;
 }
 
@@ -821,7 +826,8 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
         continue;
       }
       while (s < m && (sbeg[s] < a || (sbeg[s] == a && ssz[s] != z))) s++;
-      if (s == m) return fail(c, PFSCDC_EINVAL, "a one-segment chunk matches no segment");
+      if (s == m || sbeg[s] != a || ssz[s] != z)
+        return fail(c, PFSCDC_EINVAL, "a hash_known chunk is not one segment of the scan");
       std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * s, 32);
     }
   }

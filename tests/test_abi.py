@@ -130,3 +130,74 @@ def test_cgo_stub_matches_header():
                      "pfscdc_writer_write", "pfscdc_writer_close", "pfscdc_set_options",
                      "pfscdc_writer_set_store", "pfscdc_store_get", "pfscdc_writer_copy"):
         assert required in seen, required
+
+
+def _go_blocks():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    return [re.sub(r"//[^\n]*", "", b) for b in re.findall(r"```go\n(.*?)```", doc, flags=re.S)]
+
+
+# Go APIs newer than the reference's toolchain (go.mod:3 `go 1.16`, etc/compile/GO_VERSION
+# 1.16.4), with the release that added them
+_GO_AFTER_116 = {
+    r'"runtime/cgo"': "1.17", r"\bcgo\.(New)?Handle\b": "1.17", r"\bunsafe\.Slice\b": "1.17",
+    r"\bunsafe\.Add\b": "1.17", r"\bunsafe\.(SliceData|String|StringData)\b": "1.20",
+    r"\batomic\.(Int32|Int64|Uint32|Uint64|Bool|Pointer|Uintptr)\b": "1.19",
+    r"\bany\b": "1.18", r"\[\s*\w+\s+(any|comparable)\s*\]": "1.18",
+    r"\bstrings\.Cut\b": "1.18", r"\b(min|max|clear)\(": "1.21", r"\bslices\.|\bmaps\.": "1.21",
+}
+
+
+def test_cgo_stub_is_go116():
+    """The stub compiles under Go 1.16: no runtime/cgo.Handle, unsafe.Slice, generics or
+    later library APIs."""
+    for code in _go_blocks():
+        for pat, ver in _GO_AFTER_116.items():
+            # parameter names min/max in a signature are identifiers, not the 1.21 builtins
+            hits = [m for m in re.finditer(pat, code)
+                    if not (pat.startswith(r"\b(min|max") and code[m.start() - 1:m.start()] in ", ")]
+            assert not hits, (pat, ver, code[hits[0].start() - 40:hits[0].end() + 40])
+
+
+def test_cgo_stub_never_rehashes_on_the_host():
+    """Uploads go through CreateWithID with the GPU's Ref.Id: no client.Create( call (its
+    Hash(chunkData), client.go:57, would re-hash the ciphertext) and no chunk.Hash."""
+    code = "\n".join(_go_blocks())
+    assert not re.search(r"\bclient\.Create\(|\.Create\(g\.ctx", code)
+    assert not re.search(r"(?<![\w.])Hash\(", code)
+    assert "CreateWithID(" in code
+
+
+def _apply_hunk(text, hunk):
+    """Apply one unified-diff hunk (context/removals must match exactly) to text."""
+    old, new = [], []
+    for line in hunk.splitlines():
+        if line.startswith(("---", "+++", "@@")):
+            continue
+        tag, body = (line[:1], line[1:]) if line else (" ", "")
+        if tag in " -":
+            old.append(body)
+        if tag in " +":
+            new.append(body)
+    old_s, new_s = "\n".join(old) + "\n", "\n".join(new) + "\n"
+    assert text.count(old_s) == 1, "hunk context does not match client.go"
+    return text.replace(old_s, new_s)
+
+
+REF_CLIENT = "/root/reference/src/internal/storage/chunk/client.go"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CLIENT), reason="reference tree not present")
+def test_create_with_id_patch_applies():
+    """The one reference-side patch applies to chunk/client.go as it lies in
+    the reference, keeps Create's behaviour (Create = CreateWithID(Hash(chunkData))) and
+    leaves the hash nowhere else."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    (hunk,) = re.findall(r"```diff\n(.*?)```", doc, flags=re.S)
+    assert "a/src/internal/storage/chunk/client.go" in hunk
+    out = _apply_hunk(open(REF_CLIENT).read(), hunk)
+    assert out.count("Hash(chunkData)") == 1
+    create = out[out.index("func (c *trackedClient) Create("):out.index("func (c *trackedClient) CreateWithID(")]
+    assert "return c.CreateWithID(ctx, md, Hash(chunkData), chunkData)" in create
+    with_id = out[out.index("func (c *trackedClient) CreateWithID("):out.index("func (c *trackedClient) Get(")]
+    assert "chunkID :=" not in with_id and "c.store.Put(ctx, key, chunkData)" in with_id
