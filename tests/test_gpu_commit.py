@@ -82,3 +82,26 @@ def test_commit_refs_needs_a_cuts_only_scan():
     with pytest.raises(_lib.PfsCdcError):
         c.commit_refs(data, coffs, known)
     c.close()
+
+
+def test_commit_refs_rejects_a_known_chunk_that_is_no_segment():
+    """hash_known marks a chunk whose content hash is its one segment's; a chunk of several
+    DataRefs marked known matches no scan segment exactly and must be refused (EINVAL), not
+    given a neighbouring segment's hash."""
+    from pfs_amd import _lib
+
+    p = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+    lens = [700, 900, 1500, 20_000, 300, 300, 45_000, 800]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 17)
+    c = Chunker(ChunkParams(p.average_bits, p.seed, p.min, p.max), 0)
+    c.set_cuts_only(True)
+    c.scan(data, offs)
+    coffs, _, known = c.form_chunks()
+    multi = np.flatnonzero(known == 0)
+    assert len(multi), "the layout must form a multi-DataRef chunk"
+    bad = known.copy()
+    bad[multi[0]] = 1
+    with pytest.raises(_lib.PfsCdcError, match="not one segment"):
+        c.commit_refs(data, coffs, bad)
+    c.close()

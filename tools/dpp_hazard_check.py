@@ -34,7 +34,11 @@ for ln, line in enumerate(src, 1):
     if not inside or not t or t.startswith((";", ".", "//")):
         continue
     op, *rest = t.split(None, 1)
-    args = [a.strip() for a in rest[0].split(",")] if rest else []
+    # operands end where the DPP/SDWA modifiers start (" quad_perm:[1,2,3,0] row_mask:..."):
+    # cut them off first, or the last operand keeps the modifier text and matches no register
+    body = re.split(r"\s+(?:quad_perm|row_|bank_mask|bound_ctrl|wave_|dst_sel|src0_sel|"
+                    r"src1_sel|dst_unused|fi:|offset|sc0|sc1|nt\b)", rest[0])[0] if rest else ""
+    args = [a.strip() for a in body.split(",")] if body else []
     if op == "s_nop":
         window.append((int(args[0], 0) + 1, set()))
         continue
