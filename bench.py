@@ -108,6 +108,9 @@ def parse():
                     help="one step at a time on the GPU, the host enqueuing the next step on a "
                          "second context ordered after the current one (1/0; default: on for "
                          "the c2 put path at one step in flight)")
+    ap.add_argument("--no-create", action="store_true",
+                    help="--path commit: every BLAKE2b of processChunk (DataRef + chunk content "
+                         "hashes, one launch) but no chunk.Create (Ref.Id)")
     ap.add_argument("--commit-hash", default="fused", choices=["fused", "separate"],
                     help="--path commit: DataRef hashes in one launch with the chunks' content "
                          "hashes (pfscdc_commit_refs), or the scan's own hash pass first")
@@ -962,7 +965,10 @@ def bench_commit(args, ctx):
     world, rank, dev, cdev, params = ctx["world"], ctx["rank"], ctx["dev"], ctx["cdev"], ctx["params"]
     from pfs_amd.cdc import Chunker
 
-    args.group = 1
+    if args.config not in ("c4", "c5"):
+        args.group = 1
+    # c4/c5: --group G commits per step per GPU (auto: >= MIN_CHAINS BLAKE2b chains, as the
+    # put path), each copy the same layout over its own files
     work = workload(args, world, rank) if args.config in ("c4", "c5") else None
     if work is None:  # c2/c3 files committed as one commit: pieces per fileset
         base = workload(args, 1, 0)
@@ -976,8 +982,12 @@ def bench_commit(args, ctx):
         work.layout, work.fs_range = lay, fs
     lay, fs = work.layout, work.fs_range
     p0 = work.gbase
-    streams = (lay.fileset_begin[fs[0]:fs[1] + 1] - p0).astype(np.uint32)
+    G, per_copy = work.group, work.per_copy
+    s1 = (lay.fileset_begin[fs[0]:fs[1] + 1] - p0).astype(np.uint32)  # one copy's streams
+    streams = np.concatenate([s1[:1]] + [s1[1:] + np.uint32(g * per_copy) for g in range(G)]) \
+        if len(s1) else s1
     total = work.total
+    total0 = int(work.offs[per_copy])  # copy 0: the commit itself
     S = args.inflight if args.inflight > 0 else 1
     data = torch.empty(total, dtype=torch.uint8, device=dev)
     chunkers = [Chunker(params, device=ctx["local"]) for _ in range(S)]
@@ -1004,7 +1014,8 @@ def bench_commit(args, ctx):
         if record:
             acc["host_form_ms"] += (time.perf_counter() - h0) * 1e3
         if fused:
-            refs, chash, seghash = chunker.commit_refs(data, coffs, known)
+            refs, chash, seghash = chunker.commit_refs(data, coffs, known,
+                                                       create=not args.no_create)
             res.segments["hash"] = seghash
         else:
             refs, chash = chunker.create_refs(data, coffs, hashes, known)
@@ -1013,7 +1024,8 @@ def bench_commit(args, ctx):
             ct = chunker.last_create_timings()
             acc["create_content_hash"] += ct["content_hash"]
             acc["create_ref_id"] += ct["ref_id"]
-        lasts[k].update(res=res, coffs=coffs, known=known, refs=refs)
+        lasts[k].update(res=res, coffs=coffs, known=known, refs=refs,
+                        chash=chash if fused else None)
 
     errors = []
 
@@ -1064,21 +1076,32 @@ def bench_commit(args, ctx):
     avg = {name: sum(a[name] for a in accs) / K for name in keys}
     last = lasts[0]
     coffs, known = last["coffs"], last["known"]
-    nch = len(coffs) - 1
+    nch_all = len(coffs) - 1
+    # copy 0 (the commit itself) is what the digests and the gathered list cover: equal at
+    # every N and G
+    nch = int(np.searchsorted(coffs, np.uint64(total0), side="left")) if G > 1 else nch_all
     # the commit's chunk list: (offset in the commit stream, size, Ref.Id, Ref.Dek) per chunk
+    # (with --no-create: the content hash in place of Ref.Id, Dek zero)
     cdt = np.dtype([("offset", "<u8"), ("size", "<u8"), ("id", "u1", (32,)), ("dek", "u1", (32,))])
     crec = np.zeros(nch, dtype=cdt)
-    crec["offset"] = coffs[:-1] + np.uint64(gbyte)
-    crec["size"] = np.diff(coffs)
-    crec["id"] = last["refs"]["id"]
-    crec["dek"] = last["refs"]["dek"]
+    crec["offset"] = coffs[:nch] + np.uint64(gbyte)
+    crec["size"] = np.diff(coffs[:nch + 1])
+    if last.get("refs") is not None:
+        crec["id"] = last["refs"]["id"][:nch]
+        crec["dek"] = last["refs"]["dek"][:nch]
+    else:
+        crec["id"] = last["chash"][:nch]
     chunks = pd.gather_records(crec, device=cdev) if world > 1 else crec
+    segs0 = last["res"].segments
+    segs0 = segs0[segs0["file"] < per_copy]
     info = dict(work.info)
     info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
                          "chunk.Create)", "mem_threshold": args.mem_threshold,
                  "filesets_this_rank": fs[1] - fs[0], "pieces_this_rank": len(work.sizes),
                  "chunks_this_rank": nch, "chunks_per_commit": int(len(chunks)),
-                 "multi_dataref_chunks": int(nch - int(known.sum())),
+                 "multi_dataref_chunks": int(nch - int(known[:nch].sum())),
+                 "commits_per_step": G, "chunks_per_step": nch_all,
+                 "chunk_create": not args.no_create,
                  "commit_hash": args.commit_hash,
                  "steps_in_flight": S,
                  "parallelism": "fileset-sharded x%d, all-gather of the chunk records" % world
@@ -1086,22 +1109,27 @@ def bench_commit(args, ctx):
     ms = avg["create"]
     ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     import hashlib
+    metric = ("GiB/s device-resident pachd commit data plane (CDC + DataRef hashes + "
+              "chunk formation + chunk.Create Ref.Id)") if not args.no_create else (
+              "GiB/s device-resident CDC + every BLAKE2b of Writer.processChunk (DataRef hashes "
+              "+ chunk content hashes, writer.go:240,301-312) + chunk formation")
     out = {
-        "metric": "GiB/s device-resident pachd commit data plane (CDC + DataRef hashes + "
-                  "chunk formation + chunk.Create Ref.Id)",
+        "metric": metric,
         "value": round(float(bytes_step) * args.steps / elapsed / GIB, 3), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / K, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "scaling": work.scaling if G > 1 else "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
         "kernel_ms": {name: round(v, 4) for name, v in avg.items()},
         "commit_chunks_digest": hashlib.blake2b(chunks.tobytes(), digest_size=16).hexdigest(),
         "dataref_hashes_digest": hashlib.blake2b(
-            np.ascontiguousarray(last["res"].segments["hash"]).tobytes(), digest_size=16).hexdigest(),
+            np.ascontiguousarray(segs0["hash"]).tobytes(), digest_size=16).hexdigest(),
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),
-                     "kernel": "chunk.Create batch (content hash + dek + ChaCha20/BLAKE2b)"},
+                     "kernel": "chunk.Create batch (content hash + dek + ChaCha20/BLAKE2b)"
+                     if not args.no_create else
+                     "one BLAKE2b launch over every segment and multi-DataRef chunk"},
     }
     if S > 1:
         out["note"] = ("kernel_ms are per step on its own stream; with %d steps in flight they "
@@ -1302,6 +1330,13 @@ def commit_parity(data, work, streams, last, params, np):
     same_cuts = bool(np.array_equal(coffs[:n + 1], want))
     ok = True
     idx = np.unique(np.linspace(0, n - 1, min(8, n)).astype(int))
+    if last.get("refs") is None:  # --no-create: the chunk content hashes
+        import hashlib
+        for i in idx:
+            ok &= bytes(last["chash"][i]) == hashlib.blake2b(w.chunks[i].data,
+                                                             digest_size=32).digest()
+        return {"first_fileset_chunk_offsets_equal_oracle": same_cuts, "chunks": n,
+                "content_hashes_equal_oracle": bool(ok), "content_hashes_checked": int(len(idx))}
     for i in idx:
         rid, dek = och.create_ref_id(w.chunks[i].data)
         ok &= bytes(last["refs"][i]["id"]) == rid and bytes(last["refs"][i]["dek"]) == dek

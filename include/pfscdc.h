@@ -170,7 +170,9 @@ int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
  * (content_hashes out; a chunk with hash_known[i] != 0 is one segment, and its hash is that
  * segment's) run as one BLAKE2b launch in longest-first order, so the two independent sets of
  * serial chains share the GPU instead of running one pass after the other; then
- * chunk.Create's dek and Ref.Id as pfscdc_create_refs.  refs as pfscdc_create_refs.
+ * chunk.Create's dek and Ref.Id as pfscdc_create_refs.  refs as pfscdc_create_refs, or NULL:
+ * then only the hashes (every BLAKE2b Writer.processChunk computes, writer.go:240,301-312)
+ * and no chunk.Create.
  * Synchronous; the scan's segment list is consumed (pfscdc_segments is empty afterwards). */
 int pfscdc_commit_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,

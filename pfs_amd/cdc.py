@@ -245,11 +245,11 @@ class Chunker:
             k = n.value
             return offs[:k + 1].copy(), hashes[:k].copy(), known[:k].astype(bool)
 
-    def commit_refs(self, data, chunk_offsets: Sequence[int], hash_known):
+    def commit_refs(self, data, chunk_offsets: Sequence[int], hash_known, create: bool = True):
         """After a cuts-only scan of ``data`` and form_chunks: the DataRef hashes of the
         scan's segments and the chunks' content hashes in one launch, then chunk.Create
         (pfscdc_commit_refs).  Returns (refs REF_DTYPE[n], content_hashes uint8[n,32],
-        segment_hashes uint8[nsegs,32])."""
+        segment_hashes uint8[nsegs,32]); with create=False the hashes only (refs is None)."""
         offs = _offsets_array(chunk_offsets)
         n = len(offs) - 1
         nsegs = int(self.lib.pfscdc_num_segments(self.ctx))
@@ -263,13 +263,13 @@ class Chunker:
                                        if isinstance(data, (bytes, bytearray)) else data,
                                        dtype=np.uint8)
             ptr, nbytes, on = (arr.ctypes.data if arr.size else None), arr.size, 0
-        refs = np.zeros(max(n, 1), dtype=_lib.ref_dtype())
+        refs = np.zeros(max(n, 1), dtype=_lib.ref_dtype()) if create else None
         rc = self.lib.pfscdc_commit_refs(self.ctx, ptr, nbytes, on,
                                          offs.ctypes.data_as(C.POINTER(C.c_uint64)), n,
                                          hashes.ctypes.data, known.ctypes.data if n else None,
-                                         refs.ctypes.data, seg.ctypes.data)
+                                         refs.ctypes.data if create else None, seg.ctypes.data)
         self._check(rc, "commit_refs")
-        return refs[:n], hashes[:n], seg[:nsegs]
+        return (refs[:n] if create else None), hashes[:n], seg[:nsegs]
 
     def create_refs(self, data, chunk_offsets: Sequence[int], content_hashes=None,
                     hash_known=None):

@@ -740,7 +740,9 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
   if (c->pending) return fail(c, PFSCDC_ESTATE, "commit_refs during a pending scan");
   if (!c->scan_valid || !c->cuts_only || !c->dev_data)
     return fail(c, PFSCDC_ESTATE, "commit_refs needs the last scan made with PFSCDC_OPT_CUTS_ONLY");
-  if (!chunk_offsets || (nchunks && (!refs || !content_hashes || !hash_known)) ||
+  // refs == NULL: the content-hash half only (every BLAKE2b of writer.go:240,301-312, no
+  // chunk.Create)
+  if (!chunk_offsets || (nchunks && (!content_hashes || !hash_known)) ||
       (c->nsegs && !segment_hashes))
     return fail(c, PFSCDC_EINVAL, "NULL argument");
   if (nbytes != c->nbytes || (bytes_on_device && (const uint8_t*)bytes != c->dev_data))
@@ -833,6 +835,12 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
   }
   c->scan_valid = false;
   c->nsegs = 0;
+  if (!refs) {  // content hashes only
+    c->have_refs = false;
+    c->create_hash_ms = pass_ms;
+    c->create_ms = pass_ms;
+    return PFSCDC_OK;
+  }
   std::vector<uint8_t> all(nchunks, 1);
   const int rc = create_refs_device(c, data, nbytes, chunk_offsets, nchunks, content_hashes,
                                     all.data(), refs);
