@@ -49,7 +49,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 64-bit adds, DPP forms, carry adds: 4.1-4.3 SIMD cycles each at 2 waves per SIMD;
 # profiles/r2/valu_issue.txt): 1024 SIMDs x 2.4 GHz / 4.  Plain 32-bit VOP2 ops (xor, add,
 # shifts) issue in ~2.1 cycles, so a kernel's own mix sets its exact ceiling.
-VALU_PEAK_GIPS = 1024 * 2.4 / 4.0
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+VALU_PEAK_GIPS = SIMDS * 2.4 / 4.0
 GIB = float(1 << 30)
 C4_FILES, C4_FILE_BYTES, C4_TAIL = 10_000, 10_737_418, 2_400
 C3_BYTES = 10 * (1 << 30)
@@ -84,6 +85,11 @@ def parse():
                          "uw: host-fed UnorderedWriter with indexes; rechunk: Writer.Copy")
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
+    ap.add_argument("--uw-workers", type=int, default=0,
+                    help="--path uw: group writers in flight (PFSCDC_UW_WORKERS; default 2)")
+    ap.add_argument("--uw-group", type=int, default=0,
+                    help="--path uw: bytes of serialized filesets per group write "
+                         "(PFSCDC_UW_INFLIGHT; default 4 GiB)")
     ap.add_argument("--rechunk-writers", type=int, default=10,
                     help="rechunk: writers the file was written by (TestStableHash shape)")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
@@ -111,6 +117,9 @@ def parse():
     ap.add_argument("--no-create", action="store_true",
                     help="--path commit: every BLAKE2b of processChunk (DataRef + chunk content "
                          "hashes, one launch) but no chunk.Create (Ref.Id)")
+    ap.add_argument("--in-place", type=int, default=-1,
+                    help="--path commit: chunk.Create's ciphertext over the plaintext "
+                         "(1/0; default: when a ciphertext copy of the step would not fit)")
     ap.add_argument("--commit-hash", default="fused", choices=["fused", "separate"],
                     help="--path commit: DataRef hashes in one launch with the chunks' content "
                          "hashes (pfscdc_commit_refs), or the scan's own hash pass first")
@@ -486,7 +495,8 @@ def main():
     roofline_cdc["rolled_fraction"] = round(rolled / total, 5) if total else None
     rvalu = {}
     if tj:
-        for kern, ms in (("blake2b_kernel", hash_ms), ("cdc_scan_kernel", scan_ms)):
+        for kern, ms, mhz in (("blake2b_kernel", hash_ms, kmean.get("hash_mhz")),
+                              ("cdc_scan_kernel", scan_ms, kmean.get("scan_mhz"))):
             n = tj.get(kern + "_valu")
             if n and ms:
                 ach = n / (ms * 1e-3) / 1e9
@@ -494,6 +504,11 @@ def main():
                                "peak": VALU_PEAK_GIPS, "unit": "G wave-instr/s",
                                "frac": round(ach / VALU_PEAK_GIPS, 4), "valu_per_launch": n,
                                "source": tj["_source"]}
+                if mhz:  # the same ceiling at the clock the kernel actually ran at (DVFS)
+                    pk = SIMDS * mhz * 1e-3 / 4.0
+                    rvalu[kern].update({"clock_mhz": round(mhz, 1),
+                                        "peak_at_clock": round(pk, 1),
+                                        "frac_at_clock": round(ach / pk, 4)})
 
     info = dict(work.info)
     info.update({"steps_in_flight": S, "host_ahead": ahead,
@@ -992,8 +1007,14 @@ def bench_commit(args, ctx):
     data = torch.empty(total, dtype=torch.uint8, device=dev)
     chunkers = [Chunker(params, device=ctx["local"]) for _ in range(S)]
     fused = args.commit_hash == "fused"
+    # the ciphertext over the plaintext (PFSCDC_OPT_CTEXT_IN_PLACE) when a ciphertext copy of
+    # the step would not fit beside it: the split Ref.Id pass without a second buffer
+    _, hbm = torch.cuda.mem_get_info(dev)
+    in_place = fused and not args.no_create and (
+        args.in_place == 1 or (args.in_place < 0 and 2 * total + (16 << 30) > hbm))
     for ch in chunkers:  # the DataRef hashes join the chunk content hashes (pfscdc_commit_refs)
         ch.set_cuts_only(fused)
+        ch.set_ctext_in_place(in_place)
     fill(chunkers[0], data, work)
     poffs = work.offs
     gbyte = int(lay.offsets()[p0])  # this rank's first byte in the commit stream
@@ -1074,6 +1095,13 @@ def bench_commit(args, ctx):
         bytes_step = int(bt.item())
     K = max(args.steps, 1)
     avg = {name: sum(a[name] for a in accs) / K for name in keys}
+    if in_place:
+        # the timed steps each read the previous step's ciphertext (pseudo-random bytes, like
+        # the synthetic input); the digests and the parity check come from one more step over
+        # the synthetic commit itself, after the timed region
+        torch.cuda.synchronize()
+        fill(chunkers[0], data, work)
+        step(0, False)
     last = lasts[0]
     coffs, known = last["coffs"], last["known"]
     nch_all = len(coffs) - 1
@@ -1101,6 +1129,7 @@ def bench_commit(args, ctx):
                  "chunks_this_rank": nch, "chunks_per_commit": int(len(chunks)),
                  "multi_dataref_chunks": int(nch - int(known[:nch].sum())),
                  "commits_per_step": G, "chunks_per_step": nch_all,
+                 "ciphertext_in_place": in_place,
                  "chunk_create": not args.no_create,
                  "commit_hash": args.commit_hash,
                  "steps_in_flight": S,
@@ -1135,6 +1164,8 @@ def bench_commit(args, ctx):
         out["note"] = ("kernel_ms are per step on its own stream; with %d steps in flight they "
                        "overlap, so ms_per_step < their sum" % S)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if in_place:  # the buffer holds the verification step's ciphertext
+            fill(chunkers[0], data, work)
         out["parity"] = commit_parity(data, work, streams, last, params, np)
     if rank == 0:
         print(json.dumps(out))
@@ -1183,21 +1214,34 @@ def bench_uw(args, ctx):
     for i in range(p0, p1):
         o = int(pieces.offs[i - p0])
         views[(int(lay.file[i]), int(lay.start[i]))] = memoryview(host[o:o + int(lay.size[i])])
+    if args.uw_workers > 0:
+        os.environ["PFSCDC_UW_WORKERS"] = str(args.uw_workers)
+    if args.uw_group > 0:
+        os.environ["PFSCDC_UW_INFLIGHT"] = str(args.uw_group)
     st = pf.Storage(ctx["local"], params, args.mem_threshold)
 
     def step():
+        t = time.perf_counter()
         w = st.new_unordered_writer()
+        w.create_ms = (time.perf_counter() - t) * 1e3
         prims = pd.put_rank_filesets(w, lay, fs, lambda f: "/%016d" % f,
                                      lambda f, s, n: views[(f, s)])
-        return prims, w
+        tm = w.timings()
+        tm["writer_create"] = w.create_ms
+        nch = sum(1 for fsv in w.events for e in fsv if e[0] == "chunk" and e[1] == -1)
+        w.release()  # its data context goes back to the Storage for the next commit
+        return prims, tm, nch
 
     for _ in range(args.warmup):
         step()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    stages = {}
     for _ in range(args.steps):
-        prims, w = step()
+        prims, tm, nchunks = step()
+        for k, v in tm.items():
+            stages[k] = stages.get(k, 0.0) + v / max(args.steps, 1)
     elapsed = time.perf_counter() - t0
     bytes_step = nbytes
     if world > 1:
@@ -1211,7 +1255,6 @@ def bench_uw(args, ctx):
         [(p.additive, p.deletive, p.size_bytes) for p in prims]
     import hashlib
     K = max(args.steps, 1)
-    nchunks = sum(1 for fsv in w.events for e in fsv if e[0] == "chunk" and e[1] == -1)
     info = {"workload": "the first %d files (%d B) of %s, Put from host memory" % (
                 nf, int(offs[nf]), args.config),
             "path": "uw (host-fed UnorderedWriter -> fileset.Writer -> index.Writer)",
@@ -1232,11 +1275,32 @@ def bench_uw(args, ctx):
             b"".join(pd.encode_primitive(*g) for g in gathered), digest_size=16).hexdigest(),
         "note": "a step: the Puts (one host copy into the fileset arenas) and the grouped "
                 "GPU write of every fileset plus the indexes, then Close",
+        "stages_ms": {k: round(v, 2) for k, v in stages.items()},
+        "stages_note": "per step; put_copy on the Put thread, the rest summed over the group "
+                       "writes (background threads, %s groups in flight on their own ctxs), "
+                       "so they overlap the Puts and each other (pfscdc_uw_timings)"
+                       % os.environ.get("PFSCDC_UW_WORKERS", "2"),
     }
+    if stages.get("put_copy"):
+        out["put_copy_gb_s"] = round(nbytes / (stages["put_copy"] * 1e-3) / 1e9, 2)
+        out["host_memcpy_gb_s"] = host_memcpy_rate(torch, min(nbytes, 4 << 30))
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_memcpy_rate(torch, nbytes):
+    """The ceiling of the Put copy: a large host-to-page-locked copy on the job's threads
+    (torch's parallel CPU copy, OMP_NUM_THREADS), best of 3, GB/s."""
+    src = torch.empty(nbytes, dtype=torch.uint8).fill_(7)
+    dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    best = 0.0
+    for _ in range(3):
+        t = time.perf_counter()
+        dst.copy_(src)
+        best = max(best, nbytes / (time.perf_counter() - t) / 1e9)
+    return {"gb_s": round(best, 2), "threads": torch.get_num_threads(), "bytes": nbytes}
 
 
 def bench_rechunk(args, ctx):

@@ -131,6 +131,12 @@ const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* ctx);
  * hashes to a following pfscdc_commit_refs, which computes them in one launch together with
  * the formed chunks' content hashes. */
 #define PFSCDC_OPT_CUTS_ONLY 2u
+/* PFSCDC_OPT_CTEXT_IN_PLACE: pfscdc_commit_refs writes every chunk's ciphertext (the object
+ * chunk.Create uploads, ChaCha20_dek(chunk)) over the chunk's plaintext in the caller's device
+ * buffer, which then holds the upload stream.  The commit needs no second buffer of its size
+ * (a 200 GiB commit on one 288 GB GPU), and the Ref.Id pass can always take the split form.
+ * Needs the scan over caller-owned device bytes. */
+#define PFSCDC_OPT_CTEXT_IN_PLACE 4u
 int pfscdc_set_options(pfscdc_ctx* ctx, uint32_t options);
 /* Refs of the last completed scan, aligned with pfscdc_segments (NULL unless the scan ran
  * with PFSCDC_OPT_REF_IDS). */
@@ -233,6 +239,11 @@ int pfscdc_last_timings(pfscdc_ctx* ctx, float out[5]);
  * (s_memrealtime in the kernels), so a kernel queued behind another stream's work is not
  * charged for the wait — the per-launch duration a kernel-trace profiler reports. */
 int pfscdc_last_kernel_spans(pfscdc_ctx* ctx, float out[2]);
+/* Shader clock (MHz) the last scan's two main kernels ran at: out[0] the candidate scan,
+ * out[1] the BLAKE2b kernel; each the sum over its waves of their lifetimes in shader cycles
+ * (s_memtime) divided by the same in wall-clock ticks (s_memrealtime).  The chip lowers its
+ * clock under load, so an instruction-issue ceiling is priced at this clock. */
+int pfscdc_last_kernel_clocks(pfscdc_ctx* ctx, float out[2]);
 
 /* Pinned host memory for staging (PCIe-inclusive end-to-end path). */
 void* pfscdc_host_alloc(uint64_t nbytes);
@@ -430,6 +441,15 @@ int pfscdc_uw_destroy(pfscdc_uwriter* w);
 /* Message of the writer's sticky error (Put/Delete/Close or the background fileset write,
  * with the data ctx's last error appended); "" while there is none. */
 const char* pfscdc_uw_last_error(const pfscdc_uwriter* w);
+/* Where the writer's time went (ms, summed over its Puts and its group writes; the group
+ * writes run on background threads, two groups in flight on two ctxs by default, so the
+ * stages overlap the Puts and each other): out[0] the Puts' host copies into the fileset
+ * arenas; per grouped close of the data streams out[1] the H2D upload queued, out[2] the
+ * cuts-only scan (it waits for the upload), out[3] the chunk replay, out[4] the one BLAKE2b
+ * launch over every piece and multi-piece chunk, out[5] chunk.Create (dek, ChaCha20, Ref.Id),
+ * out[6] the data chunks' callbacks; out[7] the index writers; out[8] the group writes'
+ * wall time. */
+int pfscdc_uw_timings(const pfscdc_uwriter* w, double out[9]);
 
 /* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
 int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);

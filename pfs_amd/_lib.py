@@ -25,6 +25,7 @@ SEG_VALID = 1
 SEG_CUT = 2
 OPT_REF_IDS = 1
 OPT_CUTS_ONLY = 2
+OPT_CTEXT_IN_PLACE = 4
 
 # Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -42,13 +43,13 @@ EXPORTED = [
     "pfscdc_writer_chunk_count", "pfscdc_writer_annotation_count", "pfscdc_writer_destroy",
     "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
     "pfscdc_uw_create", "pfscdc_uw_put", "pfscdc_uw_delete", "pfscdc_uw_close",
-    "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_uw_last_error",
+    "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_uw_last_error", "pfscdc_uw_timings",
     "pfscdc_path_clean",
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
     "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
-    "pfscdc_last_kernel_spans", "pfscdc_order_hash_after",
+    "pfscdc_last_kernel_spans", "pfscdc_last_kernel_clocks", "pfscdc_order_hash_after",
 ]
 
 
@@ -182,6 +183,7 @@ def load() -> C.CDLL:
             "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
             "pfscdc_last_scan_bytes": (i32, [vp, P(u64)]),
             "pfscdc_last_kernel_spans": (i32, [vp, P(C.c_float)]),
+            "pfscdc_last_kernel_clocks": (i32, [vp, P(C.c_float)]),
             "pfscdc_set_options": (i32, [vp, u32]),
             "pfscdc_refs": (vp, [vp]),
             "pfscdc_last_ref_ms": (i32, [vp, P(C.c_float)]),
@@ -211,6 +213,7 @@ def load() -> C.CDLL:
             "pfscdc_uw_fileset": (i32, [vp, u32, P(FilesetInfo)]),
             "pfscdc_uw_destroy": (i32, [vp]),
             "pfscdc_uw_last_error": (C.c_char_p, [vp]),
+            "pfscdc_uw_timings": (i32, [vp, P(C.c_double)]),
             "pfscdc_path_clean": (i32, [C.c_char_p, i32, C.c_char_p, u64]),
             "pfscdc_hash_data_refs": (i32, [vp, vp, u32, vp]),
             "pfscdc_store_create": (i32, [P(vp)]),

@@ -65,16 +65,24 @@ class Chunker:
         self.ctx = ctx
         self.ref_ids = False
         self.cuts_only = False
+        self.ctext_in_place = False
         if ref_ids:
             self.set_ref_ids(True)
 
     def _set_options(self) -> None:
-        o = (_lib.OPT_REF_IDS if self.ref_ids else 0) | (_lib.OPT_CUTS_ONLY if self.cuts_only else 0)
+        o = (_lib.OPT_REF_IDS if self.ref_ids else 0) | (_lib.OPT_CUTS_ONLY if self.cuts_only else 0) \
+            | (_lib.OPT_CTEXT_IN_PLACE if self.ctext_in_place else 0)
         self._check(self.lib.pfscdc_set_options(self.ctx, o), "set_options")
 
     def set_ref_ids(self, on: bool) -> None:
         """Also compute each segment's Ref (Id, Dek) of chunk.Create (pfscdc.h)."""
         self.ref_ids = on
+        self._set_options()
+
+    def set_ctext_in_place(self, on: bool) -> None:
+        """commit_refs writes each chunk's ciphertext over its plaintext in the caller's
+        device tensor (PFSCDC_OPT_CTEXT_IN_PLACE)."""
+        self.ctext_in_place = on
         self._set_options()
 
     def set_cuts_only(self, on: bool) -> None:
@@ -181,6 +189,9 @@ class Chunker:
         sp = (C.c_float * 2)()
         self._check(self.lib.pfscdc_last_kernel_spans(self.ctx, sp), "kernel_spans")
         t["scan_span"], t["hash_span"] = sp[0], sp[1]
+        ck = (C.c_float * 2)()
+        self._check(self.lib.pfscdc_last_kernel_clocks(self.ctx, ck), "kernel_clocks")
+        t["scan_mhz"], t["hash_mhz"] = ck[0], ck[1]
         if self.ref_ids:
             ms = C.c_float()
             self._check(self.lib.pfscdc_last_ref_ms(self.ctx, C.byref(ms)), "timings")

@@ -341,12 +341,25 @@ PFS_DEV bool last_block_done(uint32_t* done_ctr, uint32_t* s_flag);
 
 // Exact kernel execution span for timing (bench roofline): the first wavefront to start
 // lowers span[0], the last to finish raises span[1] (s_memrealtime, the constant wall clock;
-// vector atomics).  span == nullptr: not recorded.
-PFS_DEV void span_begin(uint64_t* span) {
-  if (span && threadIdx.x == 0) atomicMin((unsigned long long*)span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+// vector atomics).  The shader clock the kernel ran at: every wave adds its lifetime in
+// shader cycles (s_memtime) to span[4] and in 100 MHz ticks (s_memrealtime) to span[5], so
+// clock = span[4] / span[5] x 100 MHz over all waves (DVFS lowers it under load: the VALU
+// issue ceiling is priced at this clock, not the nominal one).  span == nullptr: not recorded.
+struct SpanClock {
+  uint64_t t0, r0;
+};
+PFS_DEV SpanClock span_begin(uint64_t* span) {
+  const SpanClock c{__builtin_amdgcn_s_memtime(), __builtin_amdgcn_s_memrealtime()};
+  if (span && threadIdx.x == 0) atomicMin((unsigned long long*)span, (unsigned long long)c.r0);
+  return c;
 }
-PFS_DEV void span_end(uint64_t* span) {
-  if (span && (threadIdx.x & 63) == 0) atomicMax((unsigned long long*)span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+PFS_DEV void span_end(uint64_t* span, SpanClock c) {
+  if (span && (threadIdx.x & 63) == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    atomicMax((unsigned long long*)span + 1, (unsigned long long)r1);
+    atomicAdd((unsigned long long*)span + 4, (unsigned long long)(t1 - c.t0));
+    atomicAdd((unsigned long long*)span + 5, (unsigned long long)(r1 - c.r0));
+  }
 }
 
 template <bool WIDE>
@@ -356,7 +369,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr, uint32_t* __restrict__ done_ctr,
     uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries,
     const uint32_t* __restrict__ unit_skip, uint64_t* span) {
-  span_begin(span);
+  const SpanClock span_clk = span_begin(span);
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
   // images.  recs[] is zeroed before the launch; candidates are added to it directly.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -499,7 +512,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     if (last_block_done(done_ctr, s_flag))
       compact_tiles<kScanBlock>(recs, ntiles, n, entries, n_entries, s_wave);
   }
-  span_end(span);
+  span_end(span, span_clk);
 }
 
 // Which leading part of each scan work unit (a wave's 64 strips, 64 * kStrip bytes) can hold
@@ -1216,7 +1229,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks,
     uint64_t* span) {
   constexpr bool CIPHER = MODE != kModeHash;
-  span_begin(span);
+  const SpanClock span_clk = span_begin(span);
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
   // i&1 while the quad's next block (loaded into registers one iteration earlier) is written
   // to the other buffer halfway through; the wave-uniform parity makes every ds_read offset
@@ -1574,7 +1587,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     g_wave_trace[4 * w + 1] = (uint64_t)hw | ((uint64_t)xcc << 32);
     g_wave_trace[4 * w + 2] = wave_steps;
   }
-  span_end(span);
+  span_end(span, span_clk);
 }
 
 hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {

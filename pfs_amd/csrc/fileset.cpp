@@ -13,7 +13,11 @@
 //   chunk/chunk.proto, fileset/index/index.proto, chunk/util.go:25-30 (Reference)
 // Every chunk stream (the data writer of a serialized fileset and each index level) is a
 // pfscdc_writer: CDC, BLAKE2b and chunk.Create run on the GPU; this file is the bookkeeping.
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -190,32 +194,89 @@ struct pfscdc_uwriter;
 
 namespace {
 
+// Contexts the writers make for themselves (a second group writer's data ctx, one ctx per
+// index level) are kept for the next writer: a ctx owns its stream, events and grow-only
+// device staging (a group write's whole input), so making them per commit costs more than
+// the commit's small index streams.  Keyed by (device, params, options); at most
+// PFSCDC_CTX_CACHE of them (default 32; 0 turns the cache off).
+struct CtxCache {
+  std::mutex mu;
+  std::vector<std::pair<std::string, pfscdc_ctx*>> free;
+  size_t cap = [] {
+    const char* e = getenv("PFSCDC_CTX_CACHE");
+    return e ? (size_t)std::max(0, atoi(e)) : (size_t)32;
+  }();
+  static std::string key(const pfscdc_params& p, int device, uint32_t options) {
+    char b[160];
+    snprintf(b, sizeof b, "%d/%u/%lld/%lld/%lld/%u", device, p.average_bits, (long long)p.seed,
+             (long long)p.min_chunk, (long long)p.max_chunk, options);
+    return b;
+  }
+  pfscdc_ctx* take(const pfscdc_params& p, int device, uint32_t options) {
+    const std::string k = key(p, device, options);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = free.size(); i-- > 0;)
+        if (free[i].first == k) {
+          pfscdc_ctx* c = free[i].second;
+          free.erase(free.begin() + (ptrdiff_t)i);
+          return c;
+        }
+    }
+    pfscdc_ctx* c = nullptr;
+    if (pfscdc_ctx_create(&p, device, &c) != PFSCDC_OK) return nullptr;
+    if (pfscdc_set_options(c, options) != PFSCDC_OK) {
+      pfscdc_ctx_destroy(c);
+      return nullptr;
+    }
+    return c;
+  }
+  void give(pfscdc_ctx* c) {
+    if (!c) return;
+    std::unique_lock<std::mutex> lk(mu);
+    if (free.size() < cap) {
+      free.emplace_back(key(pfscdc::ctx_params(c), pfscdc::ctx_device(c), pfscdc::ctx_options(c)), c);
+      return;
+    }
+    lk.unlock();
+    pfscdc_ctx_destroy(c);
+  }
+};
+CtxCache& ctx_cache() {
+  static CtxCache* p = new CtxCache();  // never destroyed: no HIP calls in static dtors
+  return *p;
+}
+
 struct Streams {  // the ctxs of every chunk stream kind; events out
   pfscdc_ctx* data_ctx = nullptr;
+  bool own_data_ctx = false;  // a second group writer's ctx (same params, options, device)
   pfscdc_params index_params{};
   std::map<int64_t, pfscdc_ctx*> index_ctx;  // by seed (= level)
   pfscdc_uw_cb cb = nullptr;
   void* user = nullptr;
+  std::mutex* emit_mu = nullptr;  // events of concurrent group writers reach cb one at a time
   int err = 0;
 
   int emit(pfscdc_uw_event& ev, uint32_t fileset) {
     ev.fileset = fileset;
-    if (cb && cb(user, &ev) != 0) return PFSCDC_ECALLBACK;
-    return PFSCDC_OK;
+    if (!cb) return PFSCDC_OK;
+    std::unique_lock<std::mutex> lk;
+    if (emit_mu) lk = std::unique_lock<std::mutex>(*emit_mu);
+    return cb(user, &ev) != 0 ? PFSCDC_ECALLBACK : PFSCDC_OK;
   }
   pfscdc_ctx* level_ctx(int level) {
     auto it = index_ctx.find(level);
     if (it != index_ctx.end()) return it->second;
     pfscdc_params p = index_params;
     p.seed = index_params.seed + level;
-    pfscdc_ctx* c = nullptr;
-    if (pfscdc_ctx_create(&p, pfscdc::ctx_device(data_ctx), &c) != PFSCDC_OK) return nullptr;
-    pfscdc_set_options(c, PFSCDC_OPT_REF_IDS);
+    pfscdc_ctx* c = ctx_cache().take(p, pfscdc::ctx_device(data_ctx), PFSCDC_OPT_REF_IDS);
+    if (!c) return nullptr;
     index_ctx[level] = c;
     return c;
   }
   ~Streams() {
-    for (auto& kv : index_ctx) pfscdc_ctx_destroy(kv.second);
+    for (auto& kv : index_ctx) ctx_cache().give(kv.second);
+    if (own_data_ctx) ctx_cache().give(data_ctx);
   }
 };
 
@@ -375,7 +436,7 @@ struct FilesetWriter {  // fileset/writer.go:21-182
   // Add(path, tag, r) with r = the concatenation of spans of base (kept alive by the caller
   // until the data writer closes)
   int add(const std::string& path, const std::string& tag, const uint8_t* base,
-          const std::vector<Span>& spans) {
+          const std::vector<Span>& spans, const uint8_t* dev_base = nullptr) {
     IndexT* x = make(path, tag);
     int rc = check_path(idx, x);
     if (rc) return rc;
@@ -383,7 +444,8 @@ struct FilesetWriter {  // fileset/writer.go:21-182
     info.files.emplace_back(path, tag);
     rc = pfscdc_writer_annotate(cw, (uint64_t)(uintptr_t)x);
     for (const Span& sp : spans) {
-      if (!rc) rc = pfscdc::writer_write_span(cw, base + sp.off, sp.len);
+      if (!rc) rc = pfscdc::writer_write_span(cw, base + sp.off, sp.len,
+                                              dev_base ? dev_base + sp.off : nullptr);
       info.size_bytes += (int64_t)sp.len;
     }
     return rc;
@@ -462,33 +524,129 @@ struct Arena {
   uint8_t* p = nullptr;
   uint64_t cap = 0, used = 0;
   bool pinned = false;  // page-locked: the H2D upload runs at full PCIe rate
+  // The device mirror: each Put's bytes go up (async, on the writer's upload stream) right
+  // after their host copy, so a group write finds its input on the device and gathers it
+  // device to device instead of waiting for a PCIe upload of the whole group.
+  uint8_t* dev = nullptr;
+  int device = -1;
+  hipEvent_t ev = nullptr;  // the last upload into the mirror
   ~Arena() {
     if (pinned) (void)hipHostFree(p);
     else delete[] p;
+    if (dev) (void)hipFree(dev);
+    if (ev) (void)hipEventDestroy(ev);
   }
 };
 
-// memcpy split over threads for large Puts (one core copies ~10 GB/s)
-void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) {
-  constexpr uint64_t kMin = 8ull << 20;
-  static const unsigned kThreads = [] {
-    const char* e = getenv("PFSCDC_COPY_THREADS");
+// memcpy split over threads for large Puts (one core copies ~10 GB/s).  The threads are
+// persistent: a Put is typically one file of ~10 MB, and spawning 15 threads per Put cost
+// more than the copy (c4: 30-40 GB/s with spawned threads).
+// PFSCDC_COPY_THREADS, else the job's thread share (OMP_NUM_THREADS: 16 per GPU on the MI355X
+// pool, whose nproc shows the whole machine), else up to 16 hardware threads.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: its threads run until exit
+    return *p;
+  }
+  unsigned threads() const { return (unsigned)workers_.size() + 1; }
+  // dst[0, n) = src[0, n), split in parts of at least kMin / 2 over the pool and the caller
+  void copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    constexpr uint64_t kMin = 4ull << 20;
+    const unsigned t = n < kMin || workers_.empty()
+                           ? 1u
+                           : (unsigned)std::min<uint64_t>(threads(), n / (kMin / 2));
+    if (t <= 1) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    std::unique_lock<std::mutex> one(call_mu_);  // one multi-part copy at a time
+    const uint64_t part = (n / t + 4095) & ~4095ULL;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = dst;
+      src_ = src;
+      n_ = n;
+      part_ = part;
+      parts_ = t;
+      next_ = 1;  // part 0 is the caller's
+      left_ = t - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min<uint64_t>(n, part));
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_ == 0; });
+  }
+
+ private:
+  CopyPool() {
     const unsigned hw = std::thread::hardware_concurrency();
-    return e ? (unsigned)atoi(e) : std::min(8u, hw ? hw : 1u);
+    unsigned t = std::min(16u, hw ? hw : 1u);
+    if (const char* e = getenv("PFSCDC_COPY_THREADS")) t = (unsigned)std::max(1, atoi(e));
+    else if (const char* e2 = getenv("OMP_NUM_THREADS"))
+      if (atoi(e2) > 0) t = (unsigned)atoi(e2);
+    for (unsigned i = 1; i < t; i++) workers_.emplace_back([this] { run(); });
+    for (auto& w : workers_) w.detach();
+  }
+  void run() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return gen_ != seen && next_ < parts_; });
+      while (next_ < parts_) {
+        const unsigned i = next_++;
+        const uint64_t a = std::min<uint64_t>(n_, part_ * i), b = std::min<uint64_t>(n_, part_ * (i + 1));
+        uint8_t* d = dst_;
+        const uint8_t* s = src_;
+        lk.unlock();
+        if (b > a) std::memcpy(d + a, s + a, b - a);
+        lk.lock();
+        if (--left_ == 0) done_cv_.notify_all();
+      }
+      seen = gen_;
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_, done_cv_;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  uint64_t n_ = 0, part_ = 0, gen_ = 0;
+  unsigned parts_ = 0, next_ = 0, left_ = 0;
+};
+
+void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) { CopyPool::get().copy(dst, src, n); }
+
+// Page-locked arenas outlive their writer: a commit creates a fresh UnorderedWriter, and
+// page-locking 1 GB for every fileset of every commit (hipHostMalloc) costs more than the Put
+// copies themselves.  Process-wide pool, at most PFSCDC_UW_ARENA_POOL arenas (default 16).
+struct ArenaPool {
+  std::mutex mu;
+  std::vector<std::unique_ptr<Arena>> free;
+  size_t cap = [] {
+    const char* e = getenv("PFSCDC_UW_ARENA_POOL");
+    return e ? (size_t)std::max(0, atoi(e)) : (size_t)16;
   }();
-  const unsigned t = n < kMin || kThreads < 2 ? 1u : (unsigned)std::min<uint64_t>(kThreads, n / (kMin / 2));
-  if (t <= 1) {
-    std::memcpy(dst, src, n);
-    return;
+  std::unique_ptr<Arena> take(uint64_t bytes, int device) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = free.size(); i-- > 0;)
+      if (free[i]->cap == bytes && free[i]->device == device) {
+        std::unique_ptr<Arena> a = std::move(free[i]);
+        free.erase(free.begin() + (ptrdiff_t)i);
+        a->used = 0;
+        return a;
+      }
+    return nullptr;
   }
-  std::vector<std::thread> th;
-  const uint64_t part = (n / t + 4095) & ~4095ULL;
-  for (unsigned i = 1; i < t; i++) {
-    const uint64_t a = std::min<uint64_t>(n, part * i), b = std::min<uint64_t>(n, part * (i + 1));
-    if (b > a) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
+  void give(std::unique_ptr<Arena> a) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (free.size() < cap) free.push_back(std::move(a));
   }
-  std::memcpy(dst, src, std::min<uint64_t>(n, part));
-  for (auto& x : th) x.join();
+};
+ArenaPool& arena_pool() {
+  static ArenaPool* p = new ArenaPool();  // never destroyed: arenas may outlive static dtors
+  return *p;
 }
 
 struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFiles does
@@ -516,22 +674,47 @@ struct Buffer {  // buffer.go:10-106; std::map orders keys bytewise, as sortFile
 
 }  // namespace
 
-struct pfscdc_uwriter {  // unordered_writer.go:15-26
+// One background group writer: its own data ctx (so groups overlap on the GPU, each on its
+// ctx's stream) and index ctxs; the group it writes; its stage times.
+struct GroupWorker {
   Streams st;
+  std::thread th;
+  std::atomic<int> rc{PFSCDC_OK};
+  std::vector<Buffer> group;
+  double stage_ms[8] = {};  // close_group's 6 stages, [6] the index writers, [7] group wall
+};
+
+struct pfscdc_uwriter {  // unordered_writer.go:15-26
   int64_t mem_threshold = 1000000000;
   int64_t mem_available = 1000000000;
   Buffer buffer;
-  std::vector<FilesetInfo> filesets;
+  std::vector<FilesetInfo> filesets;  // by serialized fileset number (groups finish in any order)
+  std::mutex fs_mu, emit_mu;
   // Serialized buffers waiting for the GPU: up to inflight_bytes of them are written
-  // together (one scan and one chunk.Create for all their data streams).  The output equals
+  // together (one scan, one hash launch and one chunk.Create for all their data streams) by
+  // one of the group writers, round robin, while Puts continue.  The output equals
   // serializing one at a time; each fileset's chunk stream is independent.
   std::vector<Buffer> pending;
   std::vector<std::unique_ptr<Arena>> pool;  // arenas of written filesets, for reuse
   std::mutex pool_mu;
-  std::vector<Buffer> in_flight;             // the group the worker writes
-  std::thread worker;
-  std::atomic<int> worker_rc{PFSCDC_OK};  // set by the background group write
-  uint64_t pending_bytes = 0, inflight_bytes = 8ull << 30;
+  std::vector<std::unique_ptr<GroupWorker>> workers;
+  size_t next_worker = 0;
+  ~pfscdc_uwriter() {  // the written filesets' arenas serve the next writer
+    if (up_stream) {
+      (void)hipStreamSynchronize(up_stream);
+      (void)hipStreamDestroy(up_stream);
+    }
+    for (auto& a : pool)
+      if (a->pinned) arena_pool().give(std::move(a));
+  }
+  double put_copy_ms = 0;  // host copies of the Puts into the arenas
+  int device = 0;
+  bool mirror = [] {  // PFSCDC_UW_MIRROR=0: upload at group write time instead (A/B)
+    const char* e = getenv("PFSCDC_UW_MIRROR");
+    return !(e && atoi(e) == 0);
+  }();
+  hipStream_t up_stream = nullptr;  // the Puts' uploads into the arena mirrors
+  uint64_t pending_bytes = 0, inflight_bytes = 4ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
                         std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
   uint32_t next_fileset = 0;
@@ -540,25 +723,33 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   std::string errmsg;  // pfscdc_uw_last_error
 
   int fail(int rc, const char* what = nullptr) {
-    join();  // the background group write uses the data ctx (and its error string) too
+    join();  // the background group writes use the data ctxs (and their error strings) too
     if (!err) {
       err = rc;
       errmsg = std::string(what ? what : "unordered writer") + " failed (status " +
                std::to_string(rc) + ")";
-      const char* ce = pfscdc_last_error(st.data_ctx);
-      if (ce && *ce) errmsg += std::string(": ") + ce;
+      for (auto& w : workers) {
+        const char* ce = pfscdc_last_error(w->st.data_ctx);
+        if (ce && *ce) {
+          errmsg += std::string(": ") + ce;
+          break;
+        }
+      }
     }
     return err;
   }
 
   std::unique_ptr<Arena> new_arena() {
-    std::lock_guard<std::mutex> lk(pool_mu);
-    if (!pool.empty()) {
-      std::unique_ptr<Arena> a = std::move(pool.back());
-      pool.pop_back();
-      a->used = 0;
-      return a;
+    {
+      std::lock_guard<std::mutex> lk(pool_mu);
+      if (!pool.empty()) {
+        std::unique_ptr<Arena> a = std::move(pool.back());
+        pool.pop_back();
+        a->used = 0;
+        return a;
+      }
     }
+    if (auto a = arena_pool().take((uint64_t)mem_threshold, mirror ? device : -1)) return a;
     auto a = std::make_unique<Arena>();
     a->cap = (uint64_t)mem_threshold;  // a Buffer never holds more than memThreshold bytes
     if (hipHostMalloc((void**)&a->p, a->cap, hipHostMallocDefault) == hipSuccess) {
@@ -566,6 +757,16 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     } else {
       a->p = new (std::nothrow) uint8_t[a->cap];
       if (!a->p) return nullptr;
+    }
+    // a mirror only for a page-locked arena (async uploads) and while device memory lasts
+    if (mirror && a->pinned && hipSetDevice(device) == hipSuccess &&
+        hipMalloc((void**)&a->dev, a->cap) == hipSuccess) {
+      if (hipEventCreateWithFlags(&a->ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipFree(a->dev);
+        a->dev = nullptr;
+      } else {
+        a->device = device;
+      }
     }
     return a;
   }
@@ -588,56 +789,88 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
 
   // Writes one group of serialized buffers: a fileset.Writer each, their data streams
   // through one grouped close, then their indexes; the arenas go back to the pool.
-  int write_group(std::vector<Buffer>& group, uint32_t fs0) {
+  int write_group(GroupWorker& gw, std::vector<Buffer>& group, uint32_t fs0) {
+    using clk = std::chrono::steady_clock;
+    const auto g0 = clk::now();
+    Streams& st = gw.st;
     std::vector<std::unique_ptr<FilesetWriter>> fws;
     std::vector<pfscdc_writer*> cws;
+    std::vector<hipEvent_t> evs;  // the group's arena uploads
     int rc = PFSCDC_OK;
     for (size_t i = 0; i < group.size() && !rc; i++) {
       fws.push_back(std::make_unique<FilesetWriter>(&st, fs0 + (uint32_t)i));
       FilesetWriter& fw = *fws.back();
       rc = fw.open();
       const uint8_t* base = group[i].arena ? group[i].arena->p : nullptr;
+      const uint8_t* dev = group[i].arena && group[i].arena->device == pfscdc::ctx_device(st.data_ctx)
+                               ? group[i].arena->dev : nullptr;
+      if (dev) evs.push_back(group[i].arena->ev);
       for (auto& p : group[i].additive)
         for (auto& t : p.second)
-          if (!rc) rc = fw.add(p.first, t.first, base, t.second);
+          if (!rc) rc = fw.add(p.first, t.first, base, t.second, dev);
       for (auto& p : group[i].deletive)
         for (auto& t : p.second)
           if (!rc) rc = fw.del(p.first, t);
       cws.push_back(fw.cw);
     }
-    if (!rc) rc = pfscdc::writers_close_group(cws.data(), cws.size());
+    if (!rc)
+      rc = pfscdc::writers_close_group(cws.data(), cws.size(), gw.stage_ms, evs.data(), evs.size());
+    const auto g1 = clk::now();
     for (size_t i = 0; i < fws.size() && !rc; i++) {
       rc = fws[i]->finish();
-      if (!rc) filesets.push_back(std::move(fws[i]->info));
+      if (!rc) {
+        std::lock_guard<std::mutex> lk(fs_mu);
+        const size_t k = fs0 + i;
+        if (filesets.size() <= k) filesets.resize(k + 1);
+        filesets[k] = std::move(fws[i]->info);
+      }
     }
     fws.clear();
+    const auto g2 = clk::now();
+    gw.stage_ms[6] += std::chrono::duration<double, std::milli>(g2 - g1).count();
+    gw.stage_ms[7] += std::chrono::duration<double, std::milli>(g2 - g0).count();
     std::lock_guard<std::mutex> lk(pool_mu);
     for (Buffer& b : group)
       if (b.arena) pool.push_back(std::move(b.arena));
     return rc;
   }
 
-  int join() {  // waits for the group being written in the background
-    if (worker.joinable()) worker.join();
-    return worker_rc;
+  int join() {  // waits for every group being written in the background
+    int rc = PFSCDC_OK;
+    for (auto& w : workers) {
+      if (w->th.joinable()) w->th.join();
+      if (!rc) rc = w->rc;
+    }
+    return rc;
   }
 
-  // Hands the pending buffers to a background thread (async) or writes them here; at most
-  // one group is in flight, so Puts keep filling arenas while the GPU writes the last group.
+  int worker_failed() const {
+    for (const auto& w : workers)
+      if (int rc = w->rc.load()) return rc;
+    return PFSCDC_OK;
+  }
+
+  // Hands the pending buffers to the next group writer's thread (async) or writes them here;
+  // one group per writer is in flight, so Puts keep filling arenas while the GPU writes the
+  // last groups, and consecutive groups overlap on the GPU (one ctx stream each).
   int flush_pending(bool async) {
-    int rc = join();
-    if (rc || pending.empty()) return rc;
+    if (int rc = worker_failed()) return rc;
+    if (pending.empty()) return PFSCDC_OK;
+    GroupWorker& gw = *workers[next_worker];
+    next_worker = (next_worker + 1) % workers.size();
+    if (gw.th.joinable()) gw.th.join();
+    if (int rc = gw.rc.load()) return rc;
     const uint32_t fs0 = next_fileset - (uint32_t)pending.size();
-    in_flight.clear();
-    in_flight.swap(pending);
+    gw.group.clear();
+    gw.group.swap(pending);
     pending_bytes = 0;
-    if (!async) return write_group(in_flight, fs0);
-    worker = std::thread([this, fs0] { worker_rc = write_group(in_flight, fs0); });
+    if (!async) return write_group(gw, gw.group, fs0);
+    gw.th = std::thread([this, &gw, fs0] { gw.rc = write_group(gw, gw.group, fs0); });
     return PFSCDC_OK;
   }
 
   int put(const std::string& p, std::string tag, bool append, const uint8_t* data, uint64_t n) {
-    if (int rc = worker_rc.load()) return rc;  // the last group's write already failed
+    if (int rc = worker_failed()) return rc;  // a background group write already failed
     if (tag.empty()) tag = "default";
     if (!append) buffer.del(p, tag);
     std::vector<Span>* w = &buffer.add(p, tag);
@@ -648,7 +881,19 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
       if (got) {
         if (!buffer.arena && !(buffer.arena = new_arena())) return PFSCDC_ENOMEM;
         Arena& a = *buffer.arena;
+        const auto c0 = std::chrono::steady_clock::now();
         copy_parallel(a.p + a.used, data + pos, got);
+        put_copy_ms += std::chrono::duration<double, std::milli>(
+                           std::chrono::steady_clock::now() - c0).count();
+        if (a.dev) {  // on to the device while the next Puts copy
+          if (!up_stream && (hipSetDevice(device) != hipSuccess ||
+                             hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking) != hipSuccess))
+            return PFSCDC_EHIP;
+          if (hipMemcpyAsync(a.dev + a.used, a.p + a.used, got, hipMemcpyHostToDevice,
+                             up_stream) != hipSuccess ||
+              hipEventRecord(a.ev, up_stream) != hipSuccess)
+            return PFSCDC_EHIP;
+        }
         if (!w->empty() && w->back().off + w->back().len == a.used) w->back().len += got;
         else w->push_back(Span{a.used, got});
         a.used += got;
@@ -693,16 +938,39 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
   if (!data_ctx || !out || mem_threshold < 0) return PFSCDC_EINVAL;
   if (!(pfscdc::ctx_options(data_ctx) & PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
   pfscdc_uwriter* w = new pfscdc_uwriter();
-  w->st.data_ctx = data_ctx;
-  w->st.cb = cb;
-  w->st.user = user;
+  pfscdc_params ip;
   if (index_params) {
-    w->st.index_params = *index_params;
+    ip = *index_params;
   } else {  // index/writer.go:13,60: WithRollingHashConfig(20, level), default min/max
-    pfscdc_default_params(&w->st.index_params);
-    w->st.index_params.average_bits = 20;
-    w->st.index_params.seed = 0;
+    pfscdc_default_params(&ip);
+    ip.average_bits = 20;
+    ip.seed = 0;
   }
+  // group writers: the first on the caller's data ctx, the others on ctxs of their own
+  // (PFSCDC_UW_WORKERS, default 2)
+  int nworkers = 2;
+  if (const char* e = getenv("PFSCDC_UW_WORKERS")) nworkers = std::max(1, std::min(8, atoi(e)));
+  for (int k = 0; k < nworkers; k++) {
+    auto gw = std::make_unique<GroupWorker>();
+    gw->st.cb = cb;
+    gw->st.user = user;
+    gw->st.emit_mu = &w->emit_mu;
+    gw->st.index_params = ip;
+    if (k == 0) {
+      gw->st.data_ctx = data_ctx;
+    } else {
+      pfscdc_ctx* c = ctx_cache().take(pfscdc::ctx_params(data_ctx), pfscdc::ctx_device(data_ctx),
+                                       pfscdc::ctx_options(data_ctx));
+      if (!c) {
+        delete w;
+        return PFSCDC_EHIP;
+      }
+      gw->st.data_ctx = c;
+      gw->st.own_data_ctx = true;
+    }
+    w->workers.push_back(std::move(gw));
+  }
+  w->device = pfscdc::ctx_device(data_ctx);
   if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
   if (const char* e = getenv("PFSCDC_UW_INFLIGHT")) w->inflight_bytes = strtoull(e, nullptr, 10);
   *out = w;
@@ -736,7 +1004,18 @@ int pfscdc_uw_close(pfscdc_uwriter* w) {
   w->closed = true;
   int rc = w->serialize();
   if (!rc) rc = w->flush_pending(false);
+  const int jr = w->join();  // the groups still in flight on the other writers
+  if (!rc) rc = jr;
   return rc ? w->fail(rc, "Close") : PFSCDC_OK;
+}
+
+int pfscdc_uw_timings(const pfscdc_uwriter* w, double out[9]) {
+  if (!w || !out) return PFSCDC_EINVAL;
+  out[0] = w->put_copy_ms;
+  for (int k = 1; k < 9; k++) out[k] = 0;
+  for (const auto& g : w->workers)
+    for (int k = 0; k < 8; k++) out[1 + k] += g->stage_ms[k];
+  return PFSCDC_OK;
 }
 
 const char* pfscdc_uw_last_error(const pfscdc_uwriter* w) {

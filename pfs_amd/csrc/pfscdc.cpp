@@ -87,7 +87,9 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
   DevBuf<pfscdc_ref> d_refs;
   DevBuf<uint8_t> d_out;  // get_chunks: plaintext when the caller's output is on the host
-  DevBuf<uint64_t> d_span;  // kernel execution spans: scan begin/end, hash begin/end
+  // kernel execution spans: [0,1] scan begin/end, [2,3] hash begin/end; shader-clock sums
+  // [4,5] scan (cycles, 100 MHz ticks), [6,7] hash
+  DevBuf<uint64_t> d_span;
   PinnedBuf<uint64_t> h_span;
   double wall_khz = 100000.0;  // s_memrealtime ticks per ms
   DevBuf<uint32_t> d_ids;  // fill_synthetic_pieces
@@ -181,9 +183,10 @@ int validate_params(const pfscdc_params* p, std::string* why) {
   return PFSCDC_OK;
 }
 
+constexpr int kSpanSlots = 8;
 // Kernel spans start as (begin = ~0, end = 0): the kernels lower begin and raise end.
 hipError_t reset_spans(pfscdc_ctx* c, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(c->d_span.p, 0, 4 * sizeof(uint64_t), st);
+  hipError_t e = hipMemsetAsync(c->d_span.p, 0, kSpanSlots * sizeof(uint64_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_span.p, 0xFF, sizeof(uint64_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_span.p + 2, 0xFF, sizeof(uint64_t), st);
   return e;
@@ -402,8 +405,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
-  HIP_OK(c, c->d_span.ensure(4));
-  HIP_OK(c, c->h_span.ensure(5));
+  HIP_OK(c, c->d_span.ensure(kSpanSlots));
+  HIP_OK(c, c->h_span.ensure(kSpanSlots + 1));
 
   const uint8_t* data;
   if (bytes_on_device) {
@@ -520,16 +523,16 @@ int pfscdc_wait(pfscdc_ctx* c) {
       HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, total * sizeof(pfscdc_ref),
                                hipMemcpyDeviceToHost, c->stream));
   }
-  HIP_OK(c, hipMemcpyAsync(c->h_span.p, c->d_span.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                           c->stream));
+  HIP_OK(c, hipMemcpyAsync(c->h_span.p, c->d_span.p, kSpanSlots * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, c->stream));
   // the rolled-byte count now: later calls on this ctx reuse d_counts
   const bool skipped = c->scan_skipped && c->ntiles;
   if (skipped)
-    HIP_OK(c, hipMemcpyAsync(c->h_span.p + 4, c->d_counts.p + 3, sizeof(uint64_t),
+    HIP_OK(c, hipMemcpyAsync(c->h_span.p + kSpanSlots, c->d_counts.p + 3, sizeof(uint64_t),
                              hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  c->scanned_bytes = skipped ? c->h_span.p[4] : c->nbytes;
+  c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] : c->nbytes;
   c->nsegs = total;
   c->scan_valid = true;
   if (const char* wtrace = getenv("PFSCDC_WAVE_TRACE")) {  // development trace: append
@@ -561,6 +564,18 @@ int pfscdc_last_kernel_spans(pfscdc_ctx* c, float out[2]) {
   return PFSCDC_OK;
 }
 
+int pfscdc_last_kernel_clocks(pfscdc_ctx* c, float out[2]) {
+  if (!c || !out) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "scan pending");
+  out[0] = out[1] = 0.f;
+  if (!c->h_span.p) return PFSCDC_OK;
+  for (int k = 0; k < 2; k++) {  // sum of wave lifetimes: shader cycles / 100 MHz ticks
+    const uint64_t cyc = c->h_span.p[4 + 2 * k], ticks = c->h_span.p[5 + 2 * k];
+    out[k] = ticks ? (float)((double)cyc / (double)ticks * (c->wall_khz / 1000.0)) : 0.f;
+  }
+  return PFSCDC_OK;
+}
+
 int pfscdc_scan(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
                 const uint64_t* file_offsets, uint32_t nfiles) {
   int rc = pfscdc_scan_async(c, bytes, nbytes, bytes_on_device, file_offsets, nfiles);
@@ -571,7 +586,8 @@ int pfscdc_scan(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_
 uint64_t pfscdc_num_segments(const pfscdc_ctx* c) { return c ? c->nsegs : 0; }
 
 int pfscdc_set_options(pfscdc_ctx* c, uint32_t options) {
-  if (!c || (options & ~(PFSCDC_OPT_REF_IDS | PFSCDC_OPT_CUTS_ONLY))) return PFSCDC_EINVAL;
+  if (!c || (options & ~(PFSCDC_OPT_REF_IDS | PFSCDC_OPT_CUTS_ONLY | PFSCDC_OPT_CTEXT_IN_PLACE)))
+    return PFSCDC_EINVAL;
   if (c->pending) return fail(c, PFSCDC_ESTATE, "set_options during a pending scan");
   c->options = options;
   return PFSCDC_OK;
@@ -747,6 +763,9 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
     return fail(c, PFSCDC_EINVAL, "NULL argument");
   if (nbytes != c->nbytes || (bytes_on_device && (const uint8_t*)bytes != c->dev_data))
     return fail(c, PFSCDC_EINVAL, "commit_refs must get the bytes of the last scan");
+  const bool in_place = (c->options & PFSCDC_OPT_CTEXT_IN_PLACE) != 0;
+  if (in_place && !bytes_on_device)
+    return fail(c, PFSCDC_EINVAL, "PFSCDC_OPT_CTEXT_IN_PLACE needs the caller's device bytes");
   if (chunk_offsets[0] != 0 || chunk_offsets[nchunks] != nbytes)
     return fail(c, PFSCDC_EINVAL, "chunk_offsets must start at 0 and end at nbytes");
   for (uint32_t i = 0; i < nchunks; i++)
@@ -842,8 +861,10 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
     return PFSCDC_OK;
   }
   std::vector<uint8_t> all(nchunks, 1);
+  // in place: the ciphertext goes over the plaintext (every hash that reads it is done)
   const int rc = create_refs_device(c, data, nbytes, chunk_offsets, nchunks, content_hashes,
-                                    all.data(), refs);
+                                    all.data(), refs,
+                                    in_place ? const_cast<uint8_t*>(data) : nullptr);
   c->create_hash_ms = pass_ms;  // the union pass (DataRef + content hashes)
   c->create_ms += pass_ms;
   return rc;
@@ -913,7 +934,7 @@ int pfscdc_candidates(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, c->d_entries.ensure(ntiles * kTileK + 1));
   HIP_OK(c, c->d_counts.ensure(4));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
-  HIP_OK(c, c->d_span.ensure(4));
+  HIP_OK(c, c->d_span.ensure(kSpanSlots));
   const uint8_t* data;
   if (bytes_on_device) {
     data = (const uint8_t*)bytes;

@@ -74,10 +74,17 @@ int ctx_device(const pfscdc_ctx* ctx);
 // ciphertexts when ctext; both stay valid until the next call or pfscdc_ctx_destroy
 hipError_t ctx_group_buffers(pfscdc_ctx* ctx, uint64_t bytes, bool ctext, uint8_t** d,
                              uint8_t** dct);
-// pfscdc_writer_close of n writers on one ctx with one scan and one chunk.Create pass
-int writers_close_group(pfscdc_writer* const* ws, size_t n);
-// a write whose bytes stay owned by the caller until the writer flushes or closes
-int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n);
+// pfscdc_writer_close of n writers on one ctx with one scan, one hash launch (every piece and
+// multi-piece chunk) and one chunk.Create pass; stage_ms (nullable, 6 doubles) accumulates
+// upload, scan, replay, hashes, create, callbacks
+// wait_events: the group's input is on the device once these have fired (uploads made
+// during the Puts); spans with a device copy are then gathered device to device
+int writers_close_group(pfscdc_writer* const* ws, size_t n, double* stage_ms = nullptr,
+                        const hipEvent_t* wait_events = nullptr, size_t n_wait = 0);
+// a write whose bytes stay owned by the caller until the writer flushes or closes; dev
+// (nullable): the same bytes already on the writer's device
+int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n,
+                      const uint8_t* dev = nullptr);
 uint32_t ctx_options(const pfscdc_ctx* ctx);
 // the last completed scan: still readable (no create_refs / get_chunks since), its files
 bool ctx_scan_valid(const pfscdc_ctx* ctx);

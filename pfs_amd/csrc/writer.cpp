@@ -161,6 +161,7 @@ struct pfscdc_writer {
   // pending bytes held by the caller instead (writer_write_span: a fileset's Put arena);
   // their concatenation replaces buf, which stays empty while spans are pending
   std::vector<std::pair<const uint8_t*, uint64_t>> spans;
+  std::vector<const uint8_t*> span_dev;  // per span: the same bytes already on the device, or null
   uint64_t span_bytes = 0;
   std::vector<uint8_t> carry;         // ref_ids: bytes of the open chunk from earlier flushes
   std::vector<PendingFile> files;     // pending annotations, in order
@@ -345,6 +346,7 @@ void materialize(pfscdc_writer* w) {
   w->buf.reserve(w->buf.size() + w->span_bytes);
   for (auto& sp : w->spans) w->buf.insert(w->buf.end(), sp.first, sp.first + sp.second);
   w->spans.clear();
+  w->span_dev.clear();
   w->span_bytes = 0;
 }
 
@@ -605,10 +607,13 @@ namespace pfscdc {
 // writers that never flushed and buffer no Copy (each fileset's data writer at Close);
 // anything else closes one by one.  Batching keeps enough BLAKE2b chains in flight: one
 // 1e9-byte fileset of ~10 MB files has ~100 chains, far below the ~32K the GPU holds.
-int writers_close_group(pfscdc_writer* const* ws, size_t n) {
+int writers_close_group(pfscdc_writer* const* ws, size_t n, double* stage_ms,
+                        const hipEvent_t* wait_events, size_t n_wait) {
   if (n == 0) return PFSCDC_OK;
   pfscdc_ctx* ctx = ws[0]->ctx;
-  bool group = n > 1;
+  // a lone writer takes the grouped path too: its pieces and multi-piece chunks still share
+  // one hash launch (pfscdc_writer_close runs them as two passes)
+  bool group = true;
   for (size_t i = 0; i < n && group; i++) {
     const pfscdc_writer* w = ws[i];
     group = !w->err && !w->closed && w->ctx == ctx && !w->buffering && w->carry.empty() &&
@@ -651,24 +656,39 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
   if (hipSetDevice(ctx_device(ctx)) != hipSuccess ||
       ctx_group_buffers(ctx, total + 64, up, &d, &dct) != hipSuccess)
     rc = PFSCDC_ENOMEM;
+  // the upload: every writer's bytes (the spans straight from the page-locked Put arenas)
+  // queued on the ctx stream, which the scan then follows; no host wait in between
+  hipStream_t st = (hipStream_t)pfscdc_stream_handle(ctx);
+  // spans whose bytes were uploaded during the Puts (the caller's events mark them landed)
+  // are gathered device to device; the rest come from host memory
+  for (size_t e = 0; e < n_wait && !rc; e++)
+    if (hipStreamWaitEvent(st, wait_events[e], 0) != hipSuccess) rc = PFSCDC_EHIP;
   for (size_t i = 0; i < n && !rc; i++) {
     const pfscdc_writer* w = ws[i];
     uint64_t at = base[i];
     if (!w->buf.empty() &&
-        hipMemcpy(d + at, w->buf.data(), w->buf.size(), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpyAsync(d + at, w->buf.data(), w->buf.size(), hipMemcpyHostToDevice, st) != hipSuccess)
       rc = PFSCDC_EHIP;
     at += w->buf.size();
     for (size_t k = 0; k < w->spans.size() && !rc; k++) {
       const auto& sp = w->spans[k];
-      if (sp.second && hipMemcpy(d + at, sp.first, sp.second, hipMemcpyHostToDevice) != hipSuccess)
+      const uint8_t* dv = k < w->span_dev.size() ? w->span_dev[k] : nullptr;
+      if (sp.second &&
+          hipMemcpyAsync(d + at, dv ? dv : sp.first, sp.second,
+                         dv ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st) != hipSuccess)
         rc = PFSCDC_EHIP;
       at += sp.second;
     }
   }
+  if (!rc && trace && hipStreamSynchronize(st) != hipSuccess) rc = PFSCDC_EHIP;  // exact stages
   const auto t1 = now();
-  if (!rc && nfiles) rc = scan_sync(ctx, d, total, 1, offsets.data(), nfiles, 0);
+  // cut positions only: the DataRef hashes join the chunk content hashes in one launch below
+  // (the commit data plane's pfscdc_commit_refs order), so their two sets of serial BLAKE2b
+  // chains share the GPU instead of running one pass after the other
+  const bool ids = ws[0]->ref_ids;
+  if (!rc && nfiles) rc = scan_sync(ctx, d, total, 1, offsets.data(), nfiles, ids ? kScanNoHash : 0);
   const auto t2 = now();
-  // replay every writer over its own files
+  // replay every writer over its own files (piece hashes pending when the scan had none)
   if (!rc) {
     const pfscdc_segment* segs = pfscdc_segments(ctx);
     const uint64_t* begin = pfscdc_file_segment_begin(ctx);
@@ -679,14 +699,60 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
       for (size_t k = 0; k < w->files.size(); k++) {
         const size_t g = first[i] + k;
         if (!w->files[k].cont) cf.annotate(w->files[k].user);
-        for (uint64_t s = begin[g]; s < begin[g + 1]; s++) cf.piece(segs[s]);
+        for (uint64_t s = begin[g]; s < begin[g + 1]; s++) cf.piece(segs[s], ids);
       }
       cf.close();
     }
   }
-  // one chunk.Create over every writer's chunks (gaps between writers are dummy records)
   const auto t3 = now();
-  if (!rc && ws[0]->ref_ids) {
+  // every piece (DataRef.Hash, writer.go:301-312) and every multi-DataRef chunk (the content
+  // hash, writer.go:240) in one LPT-ordered launch; a one-piece chunk's hash is its piece's
+  if (!rc && ids) {
+    std::vector<uint64_t> begins, sizes;
+    std::vector<std::pair<size_t, size_t>> who;  // (writer, out) or (writer, ~event)
+    for (size_t i = 0; i < n; i++) {
+      const ChunkFormer& cf = ws[i]->cf;
+      for (size_t o = 0; o < cf.outs.size(); o++)
+        if (cf.out_pending[o]) {
+          begins.push_back(cf.out_begin[o]);
+          sizes.push_back((uint64_t)cf.outs[o].data_ref.size_bytes);
+          who.emplace_back(i, o);
+        }
+      for (size_t e = 0; e < cf.events.size(); e++)
+        if (!cf.events[e].known) {
+          begins.push_back(cf.events[e].begin);
+          sizes.push_back(cf.events[e].end - cf.events[e].begin);
+          who.emplace_back(i, ~e);
+        }
+    }
+    std::vector<uint8_t> h(32 * who.size());
+    if (!who.empty())
+      rc = hash_records_device(ctx, d, total, begins.data(), sizes.data(), (uint32_t)who.size(),
+                               h.data());
+    for (size_t k = 0; k < who.size() && !rc; k++) {
+      ChunkFormer& cf = ws[who[k].first]->cf;
+      const size_t x = who[k].second;
+      if ((intptr_t)x >= 0) {
+        std::memcpy(cf.outs[x].data_ref.hash, h.data() + 32 * k, 32);
+        cf.out_pending[x] = 0;
+      } else {
+        std::memcpy(cf.events[~x].hash, h.data() + 32 * k, 32);
+      }
+    }
+    for (size_t i = 0; i < n && !rc; i++) {
+      ChunkFormer& cf = ws[i]->cf;
+      for (ChunkEvent& ev : cf.events) {
+        if (ev.known)  // one piece: its hash (the unknown ones were hashed above)
+          for (size_t o = ev.ann_begin; o < ev.ann_end; o++)
+            if (cf.outs[o].has_data_ref) std::memcpy(ev.hash, cf.outs[o].data_ref.hash, 32);
+        ev.known = 1;  // every chunk's content hash is now known
+      }
+    }
+  }
+  const auto t4 = now();
+  // one chunk.Create (dek + Ref.Id) over every writer's chunks (gaps between writers are dummy
+  // records)
+  if (!rc && ids) {
     std::vector<uint64_t> coffs;
     std::vector<uint8_t> hashes, known;
     std::vector<std::pair<size_t, size_t>> who;  // record -> (writer, event), or gap
@@ -721,7 +787,7 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
       if (up) rc = upload(w->store, refs[r], dct, coffs[r], coffs[r + 1]);
     }
   }
-  const auto t4 = now();
+  const auto t5 = now();
   for (size_t i = 0; i < n; i++) {
     pfscdc_writer* w = ws[i];
     w->closed = true;
@@ -729,30 +795,38 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n) {
     w->buf.clear();
     w->buf.shrink_to_fit();
     w->spans.clear();
+    w->span_dev.clear();
     w->span_bytes = 0;
     if (rc) {
-      w->cf.events.clear();
-      w->cf.outs.clear();
+      clear_events(w->cf);
       set_err(w, rc);
       continue;
     }
     int r2 = callbacks(w);
     if (r2 && !rc) rc = r2;
   }
+  const auto t6 = now();
+  // stages (ms): upload queued (with PFSCDC_TRACE: landed), scan (incl. the upload when not
+  // traced), replay, hashes, chunk.Create, callbacks
+  const double stages[6] = {ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5), ms(t5, t6)};
+  if (stage_ms)
+    for (int k = 0; k < 6; k++) stage_ms[k] += stages[k];
   if (trace)
     fprintf(stderr, "[pfscdc] close_group n=%zu bytes=%lu upload %.1f ms scan %.1f replay %.1f "
-            "create %.1f callbacks %.1f\n", n, (unsigned long)total, ms(t0, t1), ms(t1, t2),
-            ms(t2, t3), ms(t3, t4), ms(t4, now()));
+            "hashes %.1f create %.1f callbacks %.1f\n", n, (unsigned long)total, stages[0],
+            stages[1], stages[2], stages[3], stages[4], stages[5]);
   return rc;
 }
 
 // Write of n caller-owned bytes kept until the writer flushes (no copy).
-int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n) {
+int writer_write_span(pfscdc_writer* w, const uint8_t* p, uint64_t n, const uint8_t* dev) {
   if (w->err) return w->err;
   if (w->closed || w->buffering || w->files.empty())
     return pfscdc_writer_write(w, p, n);  // anything unusual: the copying path
   if (n) {
     w->spans.emplace_back(p, n);
+    w->span_dev.resize(w->spans.size() - 1, nullptr);
+    w->span_dev.push_back(dev);
     w->span_bytes += n;
   }
   return PFSCDC_OK;

@@ -19,6 +19,7 @@ index streams, with its Ref.Id) and every level-0 index entry (pbutil frame).
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -56,18 +57,38 @@ class Storage:
                  index_params: Optional[ChunkParams] = None):
         self.device, self.params = device, params
         self.mem_threshold, self.index_params = mem_threshold, index_params
+        self._idle: list = []  # data-stream contexts of closed writers, for the next writer
 
     def new_unordered_writer(self) -> "UnorderedWriter":
         return UnorderedWriter(self)
+
+    def _take_chunker(self) -> Chunker:
+        # a context (stream, events, device staging) per GPU, reused writer after writer, as
+        # a pachd process would hold it; a writer still open gets a context of its own
+        return self._idle.pop() if self._idle else Chunker(self.params, self.device, ref_ids=True)
+
+    def _give_chunker(self, c: Chunker) -> None:
+        if c.ctx:  # (a context closed by its own finalizer is not reused)
+            self._idle.append(c)
 
 
 class UnorderedWriter:
     def __init__(self, storage: Storage):
         self.lib = _lib.load()
-        self._chunker = Chunker(storage.params, storage.device, ref_ids=True)
+        self._storage = storage
+        self._chunker = storage._take_chunker()
         self.events: list = []
         self._exc: Optional[BaseException] = None
-        self._cfun = _lib.UW_CB(self._on_event)
+        # the callback reaches the writer through a weak reference: a bound method here would
+        # make a reference cycle, which the cyclic GC frees in arbitrary order, closing the
+        # data context before this writer could hand it back to the Storage
+        ref = weakref.ref(self)
+
+        def on_event(user, ev_p, _ref=ref):
+            o = _ref()
+            return o._on_event(user, ev_p) if o is not None else 1
+
+        self._cfun = _lib.UW_CB(on_event)
         ip = storage.index_params.to_c() if storage.index_params else None
         w = C.c_void_p()
         rc = self.lib.pfscdc_uw_create(self._chunker.ctx, storage.mem_threshold,
@@ -111,6 +132,13 @@ class UnorderedWriter:
     def delete(self, p: str, tag: str = "") -> None:
         self._check(self.lib.pfscdc_uw_delete(self._w, p.encode(), tag.encode()), "Delete")
 
+    def timings(self) -> dict:
+        """Stage times (ms) of this writer (pfscdc_uw_timings)."""
+        out = (C.c_double * 9)()
+        self._check(self.lib.pfscdc_uw_timings(self._w, out), "timings")
+        return dict(zip(["put_copy", "upload", "scan", "replay", "hashes", "create",
+                         "callbacks", "index", "group_wall"], [round(x, 3) for x in out]))
+
     def close(self) -> list:
         self._check(self.lib.pfscdc_uw_close(self._w), "Close")
         out = []
@@ -122,12 +150,17 @@ class UnorderedWriter:
             out.append(Primitive(a, d, info.size_bytes, info.num_files, info.num_deletes))
         return out
 
+    def release(self) -> None:
+        """Destroy the writer and hand its data context back to the Storage."""
+        if getattr(self, "_w", None):
+            self.lib.pfscdc_uw_destroy(self._w)
+            self._w = None
+        if getattr(self, "_chunker", None):
+            self._storage._give_chunker(self._chunker)
+            self._chunker = None
+
     def __del__(self):
         try:
-            if getattr(self, "_w", None):
-                self.lib.pfscdc_uw_destroy(self._w)
-                self._w = None
-            if getattr(self, "_chunker", None):
-                self._chunker.close()
+            self.release()
         except Exception:
             pass

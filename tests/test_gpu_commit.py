@@ -105,3 +105,62 @@ def test_commit_refs_rejects_a_known_chunk_that_is_no_segment():
     with pytest.raises(_lib.PfsCdcError, match="not one segment"):
         c.commit_refs(data, coffs, bad)
     c.close()
+
+
+def test_commit_refs_ciphertext_in_place():
+    """PFSCDC_OPT_CTEXT_IN_PLACE: the same Refs as the copy form, and the device buffer then
+    holds every chunk's ChaCha20_dek(chunk) (transform.go:181-188), the object chunk.Create
+    uploads: BLAKE2b of it is Ref.Id (client.go:57), and the oracle's cipher gives the same
+    bytes on a sample."""
+    import torch
+
+    p = Ch.Params(average_bits=13, seed=1, min=4000, max=60000)
+    rng = np.random.default_rng(7)
+    lens = np.concatenate([rng.integers(0, 9000, 200), rng.integers(20_000, 150_000, 30)])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    host = synthetic_bytes(offs, 77)
+    nf = len(lens)
+    streams = [0, nf // 2, nf]
+    cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+    a = Chunker(cp, 0)
+    a.set_cuts_only(True)
+    ta = torch.from_numpy(host).to("cuda:0")
+    a.scan(ta, offs)
+    coffs, _, known = a.form_chunks(streams)
+    refs_a, chash_a, seg_a = a.commit_refs(ta, coffs, known)
+    assert torch.equal(ta.cpu(), torch.from_numpy(host)), "the copy form left the input alone"
+    b = Chunker(cp, 0)
+    b.set_cuts_only(True)
+    b.set_ctext_in_place(True)
+    tb = torch.from_numpy(host).to("cuda:0")
+    b.scan(tb, offs)
+    coffs_b, _, known_b = b.form_chunks(streams)
+    refs_b, chash_b, seg_b = b.commit_refs(tb, coffs_b, known_b)
+    assert np.array_equal(refs_b["id"], refs_a["id"]) and np.array_equal(refs_b["dek"], refs_a["dek"])
+    assert np.array_equal(chash_b, chash_a) and np.array_equal(seg_b, seg_a)
+    ct = tb.cpu().numpy()
+    for i in range(len(coffs) - 1):
+        c = ct[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        assert hashlib.blake2b(c, digest_size=32).digest() == bytes(refs_b[i]["id"]), i
+    for i in np.linspace(0, len(coffs) - 2, 6).astype(int):
+        plain = host[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        assert ct[int(coffs[i]):int(coffs[i + 1])].tobytes() == Ch.chacha20_xor(
+            bytes(refs_b[i]["dek"]), plain), i
+    a.close()
+    b.close()
+
+
+def test_ciphertext_in_place_needs_device_bytes():
+    from pfs_amd import _lib
+
+    p = Ch.Params(average_bits=12, seed=1, min=2000, max=30000)
+    offs = np.array([0, 50_000, 90_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 5)
+    c = Chunker(ChunkParams(p.average_bits, p.seed, p.min, p.max), 0)
+    c.set_cuts_only(True)
+    c.set_ctext_in_place(True)
+    c.scan(data, offs)
+    coffs, _, known = c.form_chunks()
+    with pytest.raises(_lib.PfsCdcError, match="device bytes"):
+        c.commit_refs(data, coffs, known)
+    c.close()

@@ -183,6 +183,18 @@ segs = pd.stream_segments(local, n, (0, n), 0, p.min, p.max,
 want, _ = coracle.segment_files(s, [0, n], p)
 for f in ("offset", "size", "flags", "hash"):
     assert np.array_equal(segs[f], want[f]), f
+# the border copy of stream_segments (distributed.py: batch_isend_irecv of device slices of
+# `local` into the room after the next range) through RCCL itself: at world size 1 the plan
+# has no border, so send a straddling segment's tail to ourselves the same way
+tail = local[1_000_000:1_000_000 + p.max]  # a forced max-size segment's worth
+room = local[n:n + p.max]
+room.zero_()
+reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, tail.contiguous(), 0),
+                               dist.P2POp(dist.irecv, room, 0)])
+for r in reqs:
+    r.wait()
+torch.cuda.synchronize()
+assert torch.equal(room, tail), "RCCL self send/recv of the border bytes"
 dist.destroy_process_group()
 print("rccl ok", len(segs))
 """ % ROOT
