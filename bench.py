@@ -86,10 +86,10 @@ def parse():
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
     ap.add_argument("--uw-workers", type=int, default=0,
-                    help="--path uw: group writers in flight (PFSCDC_UW_WORKERS; default 2)")
+                    help="--path uw: group writers in flight (PFSCDC_UW_WORKERS; default 1)")
     ap.add_argument("--uw-group", type=int, default=0,
                     help="--path uw: bytes of serialized filesets per group write "
-                         "(PFSCDC_UW_INFLIGHT; default 4 GiB)")
+                         "(PFSCDC_UW_INFLIGHT; default 8 GiB)")
     ap.add_argument("--rechunk-writers", type=int, default=10,
                     help="rechunk: writers the file was written by (TestStableHash shape)")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,
@@ -1277,9 +1277,9 @@ def bench_uw(args, ctx):
                 "GPU write of every fileset plus the indexes, then Close",
         "stages_ms": {k: round(v, 2) for k, v in stages.items()},
         "stages_note": "per step; put_copy on the Put thread, the rest summed over the group "
-                       "writes (background threads, %s groups in flight on their own ctxs), "
+                       "writes (a background thread per group writer, %s writer(s), each on its own ctx), "
                        "so they overlap the Puts and each other (pfscdc_uw_timings)"
-                       % os.environ.get("PFSCDC_UW_WORKERS", "2"),
+                       % os.environ.get("PFSCDC_UW_WORKERS", "1"),
     }
     if stages.get("put_copy"):
         out["put_copy_gb_s"] = round(nbytes / (stages["put_copy"] * 1e-3) / 1e9, 2)

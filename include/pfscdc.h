@@ -441,9 +441,9 @@ int pfscdc_uw_destroy(pfscdc_uwriter* w);
 /* Message of the writer's sticky error (Put/Delete/Close or the background fileset write,
  * with the data ctx's last error appended); "" while there is none. */
 const char* pfscdc_uw_last_error(const pfscdc_uwriter* w);
-/* Where the writer's time went (ms, summed over its Puts and its group writes; the group
- * writes run on background threads, two groups in flight on two ctxs by default, so the
- * stages overlap the Puts and each other): out[0] the Puts' host copies into the fileset
+/* Where the writer's time went (ms, summed over its Puts and its group writes; a group
+ * write runs on a background thread while Puts continue (PFSCDC_UW_WORKERS > 1: several
+ * groups in flight, each on a ctx of its own), so the stages overlap the Puts: out[0] the Puts' host copies into the fileset
  * arenas; per grouped close of the data streams out[1] the H2D upload queued, out[2] the
  * cuts-only scan (it waits for the upload), out[3] the chunk replay, out[4] the one BLAKE2b
  * launch over every piece and multi-piece chunk, out[5] chunk.Create (dek, ChaCha20, Ref.Id),
