@@ -558,6 +558,10 @@ def main():
                                     "note": "median of 3 steps with nothing else in flight, "
                                             "after the timed region"}
 
+    if args.config in ("c4", "c5") and work.group > 1:
+        # the literal configuration beside the grouped one: ONE commit per step over the N GPUs
+        # (copy 0 of this rank's share: strong scaling, bound by its longest chains)
+        out["single_commit"] = single_commit(args, work, chunkers[0], batches[0], ctx)
     if gather and rank == 0 and "index" in last:
         idx = last["index"]
         if args.config in ("c4", "c5"):  # the commit itself: copy 0 of every rank
@@ -597,6 +601,45 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     chunker.close()
+
+
+def single_commit(args, work, chunker, data, ctx):
+    """One commit per step (G = 1) on the same ranks and contexts: the step time of the
+    configured 100 GiB commit itself over N GPUs (strong scaling), max over ranks."""
+    torch, dist, world, cdev = ctx["torch"], ctx["dist"], ctx["world"], ctx["cdev"]
+    offs0 = work.offs[:work.per_copy + 1]
+    total0 = int(offs0[-1])
+    part = data[:total0]
+    for _ in range(max(1, args.warmup)):
+        chunker.scan_async(part, offs0)
+        chunker.wait()
+    k = max(2, min(args.steps, 4))
+    hs = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        chunker.scan_async(part, offs0)
+        chunker.wait()
+        hs.append(chunker.timings()["hash_span"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    nb = float(total0)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        bt = torch.tensor([nb], dtype=torch.float64, device=cdev)
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        nb = float(bt.item())
+    return {"value": round(nb * k / el / GIB, 3), "unit": "GiB/s", "ms_per_step": round(el * 1e3 / k, 3),
+            "steps": k, "commits_per_step": 1, "scaling": "strong",
+            "hash_span_ms_median": med(hs),
+            "note": "the same ranks with one commit per step instead of %d: bound by the serial "
+                    "BLAKE2b chains of the commit's ~10.7 MB files on each GPU" % work.group}
 
 
 def chain_floor(res, hash_ms, data, params, local, Chunker):
