@@ -1165,6 +1165,9 @@ def bench_commit(args, ctx):
     chunks = pd.gather_records(crec, device=cdev) if world > 1 else crec
     segs0 = last["res"].segments
     segs0 = segs0[segs0["file"] < per_copy]
+    dr_hashes = np.ascontiguousarray(segs0["hash"]).view(np.dtype((np.void, 32))).reshape(-1)
+    if world > 1:  # the commit's DataRef hashes in commit order: equal at every N
+        dr_hashes = pd.gather_records(dr_hashes, device=cdev)
     info = dict(work.info)
     info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
                          "chunk.Create)", "mem_threshold": args.mem_threshold,
@@ -1194,8 +1197,7 @@ def bench_commit(args, ctx):
         "data": "synthetic (seeded splitmix64 bytes generated in HBM)", "config": info,
         "kernel_ms": {name: round(v, 4) for name, v in avg.items()},
         "commit_chunks_digest": hashlib.blake2b(chunks.tobytes(), digest_size=16).hexdigest(),
-        "dataref_hashes_digest": hashlib.blake2b(
-            np.ascontiguousarray(segs0["hash"]).tobytes(), digest_size=16).hexdigest(),
+        "dataref_hashes_digest": hashlib.blake2b(dr_hashes.tobytes(), digest_size=16).hexdigest(),
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                      "bytes_per_launch": total, "avg_launch_ms": round(ms, 4),

@@ -142,3 +142,32 @@ def test_reference_index_params_many_small_files_multilevel():
     levels = {e[2] for e in wlog[0] if e[0] == "chunk" and e[1] == 0}
     assert max(levels) >= 1, levels
     check(want, got, wlog, glog)
+
+
+@pytest.mark.parametrize("workers,mirror", [("2", "1"), ("3", "0"), ("1", "0")])
+def test_group_writers_and_upload_paths(workers, mirror, monkeypatch):
+    """Round-3 write path: several groups in flight on group writers of their own ctxs
+    (PFSCDC_UW_WORKERS), Put bytes uploaded into arena device mirrors as they arrive or
+    uploaded at group time (PFSCDC_UW_MIRROR), the union hash launch per grouped close: the
+    output must equal the restated reference whatever the grouping and upload path."""
+    monkeypatch.setenv("PFSCDC_UW_INFLIGHT", "300000")
+    monkeypatch.setenv("PFSCDC_UW_WORKERS", workers)
+    monkeypatch.setenv("PFSCDC_UW_MIRROR", mirror)
+    ops, _ = workload(3, 160, 40_000)
+    want, got, wlog, glog = run_both(ops, SMALL, 400_000, SMALL_INDEX)
+    assert len(want) >= 5
+    check(want, got, wlog, glog)
+
+
+@pytest.mark.parametrize("workers", ["1", "2"])
+def test_large_puts_copy_pool_reference_params(workers, monkeypatch):
+    """Puts above the copy pool's 4 MiB split (the persistent copy threads) and files split
+    across filesets, at the reference's chunking; one and two group writers."""
+    monkeypatch.setenv("PFSCDC_UW_WORKERS", workers)
+    monkeypatch.setenv("PFSCDC_UW_INFLIGHT", "15000000")
+    data = synthetic_bytes([0, 40 << 20], 11).tobytes()
+    ops = [("put", f"/f{i}", "", False, data[i * (9 << 20):(i + 1) * (9 << 20)]) for i in range(4)]
+    ops.append(("put", "/g", "", False, data[36 << 20:]))
+    want, got, wlog, glog = run_both(ops, Ch.Params(), 10_000_000)
+    assert len(want) == 5
+    check(want, got, wlog, glog)
