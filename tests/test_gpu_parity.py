@@ -246,3 +246,22 @@ def test_scan_skip_c2_layout_rolls_three_quarters():
     assert_same(c.scan(data, offs), data, offs, p)
     per_file = (4 << 20) - (999_999 // 8192) * 8192
     assert c.last_scan_bytes() == 8 * per_file
+
+
+def test_kernel_spans_and_clocks_are_recorded():
+    """The execution spans and the shader clock of the scan and hash kernels (s_memtime /
+    s_memrealtime per wave, pfscdc_last_kernel_clocks) come back with every scan: spans
+    positive and within the HIP-event intervals, clocks within the chip's range."""
+    import torch
+
+    offs = np.arange(0, 65, dtype=np.uint64) * np.uint64(4 << 20)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda:0")
+    c = Chunker(cp(DEFAULT), 0)
+    c.fill_synthetic(t, offs, 3)
+    res = c.scan(t, offs)
+    assert len(res.segments) >= 64
+    tm = c.timings()
+    assert 0 < tm["scan_span"] <= tm["scan"] + 0.05 and 0 < tm["hash_span"] <= tm["hash"] + 0.05
+    for k in ("scan_mhz", "hash_mhz"):
+        assert 400 < tm[k] < 3000, (k, tm[k])
+    c.close()
