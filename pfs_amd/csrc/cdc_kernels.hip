@@ -1615,7 +1615,8 @@ PFS_DEV uint32_t rotl32v(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x
 __global__ __launch_bounds__(256) void chacha_xor_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
     const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
-    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out) {
+    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);  // the long chunk set's pass issues first
   const uint64_t nblocks = blk_base[n];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint32_t lane = threadIdx.x & 63u;
@@ -2083,12 +2084,12 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st, int waves) {
+                          uint8_t* ctext_out, hipStream_t st, int waves, uint32_t prio) {
   if (max_segments == 0) return hipSuccess;
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
-      data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out, hash_prio_blocks(),
-      nullptr);
+      data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
+      prio ? prio : hash_prio_blocks(), nullptr);
   return hipGetLastError();
 }
 
@@ -2101,11 +2102,15 @@ hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t
 
 hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pfscdc_segment* segs,
                              const uint64_t* blk_base, uint32_t n, uint64_t nblocks,
-                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st) {
+                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st,
+                             bool prio, bool one_wave_per_simd) {
   if (nblocks == 0) return hipSuccess;
-  const uint64_t need = (nblocks + 255) / 256, full = (uint64_t)num_cus * 32;
-  chacha_xor_kernel<<<(unsigned)(need < full ? need : full), 256, 0, st>>>(data, offs, segs,
-                                                                          blk_base, n, refs, out);
+  // one_wave_per_simd: num_cus workgroups of 4 waves (room left on every SIMD for another
+  // context's launches)
+  const uint64_t need = (nblocks + 255) / 256,
+                 full = (uint64_t)num_cus * (one_wave_per_simd ? 1 : 32);
+  chacha_xor_kernel<<<(unsigned)(need < full ? need : full), 256, 0, st>>>(
+      data, offs, segs, blk_base, n, refs, out, prio ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "pfscdc_internal.h"
 
 using namespace pfscdc;
@@ -62,6 +64,14 @@ struct PinnedBuf {
   }
 };
 
+// create_refs_device(finish = false) -> create_refs_finish: what the second half unpacks
+struct CreatePending {
+  bool active = false, split = false;
+  uint32_t k = 0, nr = 0;
+  uint8_t* hashes = nullptr;
+  pfscdc_ref* refs = nullptr;
+};
+
 }  // namespace
 
 struct pfscdc_ctx {
@@ -109,6 +119,15 @@ struct pfscdc_ctx {
   hipStream_t aux_stream = nullptr;      // create_refs: the second Ref.Id stream (lazy)
   hipEvent_t xev[2] = {nullptr, nullptr};  // its fork / join events
   std::vector<uint32_t> perm;  // create_refs: record -> chunk
+  CreatePending cr;            // create_refs enqueued, not yet finished
+  // create_refs launch shape for this call (commit_refs' two chunk sets): waves per SIMD cap
+  // (0: none; also caps the ChaCha20 grid at one wave per SIMD), issue priority of every hash
+  // launch (0: the launch's own), ChaCha20 waves at issue priority 2
+  int cr_wave_cap = 0;
+  uint32_t cr_hash_prio = 0;
+  bool cr_chacha_prio = false;
+  pfscdc_ctx* helper = nullptr;  // commit_refs: the short chunk set's context (lazy)
+  hipEvent_t pev[3] = {nullptr, nullptr, nullptr};  // commit_refs: start, long / short unions
   bool have_refs = false;
   bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
@@ -314,6 +333,9 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   if (c->wev) (void)hipEventDestroy(c->wev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+  for (auto& e : c->pev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->helper) pfscdc_ctx_destroy(c->helper);
   for (auto& e : c->xev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -749,6 +771,185 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
                             refs);
 }
 
+// pfscdc_commit_refs in two chunk sets (PFSCDC_COMMIT_TWO_SETS=0: one union pass over every
+// record, then one Ref.Id pass, A/B).  A chunk's Ref.Id needs only its own content hash, and
+// the commit's critical path is the longest chunks' two serial chains (content hash, then the
+// BLAKE2b of its ciphertext, writer.go:240 + client.go:57).  So the chunks longer than
+// PFSCDC_COMMIT_LONG_PCT (default 50) percent of the longest, with every segment inside them,
+// form the long set on this ctx's stream: their hashes, then at once their deks, ChaCha20 and
+// Ref.Id chains, at issue priority 2.  The rest (segments, content hashes and chunk.Create of
+// the shorter chunks) runs on a helper ctx's stream beside them, at one wave per SIMD so the
+// long set's launches always find room on every SIMD.  The two sets read and (in place)
+// write disjoint bytes.  Returns kOnePass when the chunk list does not allow it.
+constexpr int kOnePass = 1;
+constexpr uint32_t kNoPrio = 0x40000000u;  // hash launch prio_blocks: never raise priority
+
+// read at every call (tests switch them per call)
+static bool commit_two_sets() {
+  const char* e = getenv("PFSCDC_COMMIT_TWO_SETS");
+  return !(e && atoi(e) == 0);
+}
+static uint64_t commit_long_pct() {
+  const char* e = getenv("PFSCDC_COMMIT_LONG_PCT");
+  const int x = e ? atoi(e) : 0;
+  return (uint64_t)(x > 0 && x < 100 ? x : 50);
+}
+
+static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
+                                const std::vector<uint64_t>& sbeg, const std::vector<uint64_t>& ssz,
+                                const uint64_t* co, uint32_t nchunks, uint8_t* content_hashes,
+                                const uint8_t* hash_known, pfscdc_ref* refs,
+                                uint8_t* segment_hashes, uint8_t* ct) {
+  if (!commit_two_sets() || nchunks < 2) return kOnePass;
+  const uint64_t m = sbeg.size();
+  // the chunk holding each segment; the segment a one-segment chunk's content hash is
+  std::vector<uint32_t> seg_chunk(m);
+  std::vector<int64_t> known_seg(nchunks, -1);
+  for (uint64_t s = 0; s < m; s++) {
+    const uint64_t a = sbeg[s], z = ssz[s];
+    uint32_t i = (uint32_t)(std::upper_bound(co, co + nchunks, a) - co);
+    i = i ? i - 1 : 0;
+    while (z > 0 && i > 0 && co[i + 1] <= a) i--;
+    if (co[i] > a || a + z > co[i + 1]) return kOnePass;  // not inside one chunk
+    seg_chunk[s] = i;
+    if (hash_known[i] && known_seg[i] < 0 && a == co[i] && z == co[i + 1] - co[i])
+      known_seg[i] = (int64_t)s;
+  }
+  uint64_t longest = 0;
+  for (uint32_t i = 0; i < nchunks; i++) {
+    if (hash_known[i] && known_seg[i] < 0) return kOnePass;  // the one-pass form reports it
+    longest = std::max(longest, co[i + 1] - co[i]);
+  }
+  const uint64_t thr = longest * commit_long_pct() / 100;
+  std::vector<uint8_t> set_of(nchunks);  // 0: long, 1: short
+  uint32_t nlong = 0;
+  for (uint32_t i = 0; i < nchunks; i++) {
+    set_of[i] = co[i + 1] - co[i] > thr ? 0 : 1;
+    nlong += set_of[i] == 0;
+  }
+  if (nlong == 0 || nlong == nchunks) return kOnePass;
+  if (!c->helper && pfscdc_ctx_create(&c->params, c->device, &c->helper) != PFSCDC_OK) {
+    c->helper = nullptr;
+    return kOnePass;
+  }
+  for (auto& e : c->pev)
+    if (!e) HIP_OK(c, hipEventCreate(&e));
+  pfscdc_ctx* const X[2] = {c, c->helper};
+  // per set: its chunks; its union records (content hashes of its multi-DataRef chunks, then
+  // every segment inside its chunks)
+  std::vector<uint32_t> sel[2], rec_chunk[2];
+  std::vector<uint64_t> rec_seg[2];
+  for (uint32_t i = 0; i < nchunks; i++) {
+    sel[set_of[i]].push_back(i);
+    if (!hash_known[i]) rec_chunk[set_of[i]].push_back(i);
+  }
+  for (uint64_t s = 0; s < m; s++) rec_seg[set_of[seg_chunk[s]]].push_back(s);
+  HIP_OK(c, hipEventRecord(c->pev[0], c->stream));  // the scan and the bytes are ready
+  HIP_OK(c, hipStreamWaitEvent(X[1]->stream, c->pev[0], 0));
+  for (int x = 0; x < 2; x++) {
+    pfscdc_ctx* u = X[x];
+    hipStream_t st = u->stream;
+    const uint64_t kc = rec_chunk[x].size(), R = kc + rec_seg[x].size();
+    HIP_OK(c, u->h_segs.ensure(R ? R : 1));
+    HIP_OK(c, u->h_offs.ensure(1));
+    HIP_OK(c, u->h_seg_begin.ensure(1));
+    HIP_OK(c, u->d_offs.ensure(1));
+    HIP_OK(c, u->d_segs.ensure(R ? R : 1));
+    HIP_OK(c, u->d_order.ensure(R ? R : 1));
+    HIP_OK(c, u->d_qctr.ensure(2));
+    HIP_OK(c, u->d_counts.ensure(4));
+    u->h_offs.p[0] = 0;
+    u->h_seg_begin.p[0] = R;
+    uint64_t lg = 0, sum = 0;
+    for (uint64_t r = 0; r < R; r++) {
+      pfscdc_segment& g = u->h_segs.p[r];
+      std::memset(&g, 0, sizeof g);
+      if (r < kc) {
+        const uint32_t i = rec_chunk[x][r];
+        g.offset = co[i];
+        g.size = co[i + 1] - co[i];
+      } else {
+        const uint64_t s = rec_seg[x][r - kc];
+        g.offset = sbeg[s];
+        g.size = ssz[s];
+      }
+      g.flags = PFSCDC_SEG_VALID;
+      lg = std::max(lg, g.size);
+      sum += g.size;
+    }
+    HIP_OK(c, hipMemcpyAsync(u->d_offs.p, u->h_offs.p, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    if (R)
+      HIP_OK(c, hipMemcpyAsync(u->d_segs.p, u->h_segs.p, sizeof(pfscdc_segment) * R,
+                               hipMemcpyHostToDevice, st));
+    HIP_OK(c, hipMemcpyAsync(u->d_counts.p + 1, u->h_seg_begin.p, sizeof(uint64_t),
+                             hipMemcpyHostToDevice, st));
+    const int w = hash_waves(lg, sum, u->num_cus);
+    if (R)
+      HIP_OK(c, launch_blake2b(data, u->d_offs.p, u->d_segs.p, u->d_counts.p + 1, R, u->d_order.p,
+                               u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
+                               x ? 1 : w, x ? kNoPrio : 1u));
+    if (R)
+      HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
+                               hipMemcpyDeviceToHost, st));
+    HIP_OK(c, hipEventRecord(c->pev[1 + x], st));
+  }
+  // as each set's hashes land: its content hashes, then its chunk.Create on its own stream
+  std::vector<uint8_t> all(nchunks, 1);
+  bool done[2] = {false, false};
+  while (!done[0] || !done[1]) {
+    bool progressed = false;
+    for (int x = 0; x < 2; x++) {
+      if (done[x]) continue;
+      const hipError_t q = hipEventQuery(c->pev[1 + x]);
+      if (q == hipErrorNotReady) continue;
+      HIP_OK(c, q);
+      pfscdc_ctx* u = X[x];
+      const uint64_t kc = rec_chunk[x].size();
+      for (uint64_t r = 0; r < kc; r++)
+        std::memcpy(content_hashes + 32ull * rec_chunk[x][r], u->h_segs.p[r].hash, 32);
+      for (uint64_t r = 0; r < rec_seg[x].size(); r++)
+        std::memcpy(segment_hashes + 32 * rec_seg[x][r], u->h_segs.p[kc + r].hash, 32);
+      for (uint32_t i : sel[x])
+        if (hash_known[i])
+          std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * known_seg[i], 32);
+      u->cr_wave_cap = x ? 1 : 0;
+      u->cr_hash_prio = x ? kNoPrio : 1u;
+      u->cr_chacha_prio = x == 0;
+      const int rc = create_refs_device(u, data, nbytes, co, nchunks, content_hashes, all.data(),
+                                        refs, ct, sel[x].data(), (uint32_t)sel[x].size(), false);
+      u->cr_wave_cap = 0;
+      u->cr_hash_prio = 0;
+      u->cr_chacha_prio = false;
+      if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(X[1]->stream);
+        if (x) c->err = X[1]->err;
+        return rc;
+      }
+      done[x] = progressed = true;
+    }
+    if (!progressed && !(done[0] && done[1])) usleep(50);
+  }
+  const int r1 = create_refs_finish(X[1]);
+  const int r0 = create_refs_finish(c);
+  if (r1) {
+    c->err = X[1]->err;
+    return r1;
+  }
+  if (r0) return r0;
+  float ms = 0.f, a = 0.f, b = 0.f;
+  for (int x = 0; x < 2; x++)
+    if (hipEventElapsedTime(&ms, c->pev[0], c->pev[1 + x]) == hipSuccess) a = std::max(a, ms);
+  for (int x = 0; x < 2; x++)
+    if (hipEventElapsedTime(&ms, c->pev[0], X[x]->ev[6]) == hipSuccess) b = std::max(b, ms);
+  c->create_hash_ms = a;  // both sets' hashes (they overlap the long set's Ref.Id pass)
+  c->create_ms = b;
+  c->scan_valid = false;
+  c->nsegs = 0;
+  c->have_refs = false;
+  return PFSCDC_OK;
+}
+
 int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,
                        const uint8_t* hash_known, pfscdc_ref* refs, uint8_t* segment_hashes) {
@@ -781,6 +982,21 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
     const pfscdc_segment& g = c->h_segs.p[s];
     sbeg[s] = c->h_offs.p[g.file] + g.offset;
     ssz[s] = g.size;
+  }
+  if (refs) {
+    // a ciphertext buffer both chunk sets write (in place: the plaintext itself)
+    uint8_t* ct = in_place ? const_cast<uint8_t*>(data) : nullptr;
+    size_t free_b = 0, total_b = 0;
+    if (!ct && (c->d_ctext.cap >= nbytes ||
+                (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                 free_b + c->d_ctext.cap >= nbytes + (8ull << 30))) &&
+        c->d_ctext.ensure(nbytes ? nbytes : 1, true) == hipSuccess)
+      ct = c->d_ctext.p;
+    if (ct) {
+      const int rc = commit_refs_two_sets(c, data, nbytes, sbeg, ssz, chunk_offsets, nchunks,
+                                          content_hashes, hash_known, refs, segment_hashes, ct);
+      if (rc != kOnePass) return rc;
+    }
   }
   // one record list: the chunks whose content hash is unknown, then every segment; all
   // absolute (file 0, offs = {0}), hashed in one LPT-ordered launch
@@ -1210,21 +1426,34 @@ static bool refid_split(uint32_t n, int num_cus) {
 // (chunk)) (cryptoXOR :181-188; the id the chunk client stores it under, client.go:57).
 // One record per chunk (file = chunk index, offset 0, over offs).  Chunks whose content hash
 // is not known come first so that one hash pass over records [0, k) computes them; the
-// Ref.Id pass then runs over all n records in its own LPT order.
+// Ref.Id pass then runs over all records in its own LPT order.  sel (nullable): only the
+// chunks sel[0..nsel) (indices into offs / hashes / known / refs).  finish = false: enqueue
+// only; create_refs_finish() waits and fills hashes / refs.
 int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, const uint64_t* offs,
                        uint32_t n, uint8_t* hashes, const uint8_t* known, pfscdc_ref* refs,
-                       uint8_t* ctext_out) {
+                       uint8_t* ctext_out, const uint32_t* sel, uint32_t nsel, bool finish) {
   if (c->pending) return fail(c, PFSCDC_ESTATE, "create_refs during a pending scan");
-  if (n == 0) return PFSCDC_OK;
+  const uint32_t nr = sel ? nsel : n;  // records
+  c->cr = CreatePending{};
+  if (nr == 0) return PFSCDC_OK;
   c->scan_valid = false;
   HIP_OK(c, hipSetDevice(c->device));
   hipStream_t st = c->stream;
-  c->perm.resize(n);
+  auto chunk_of = [&](uint32_t t) { return sel ? sel[t] : t; };
+  c->perm.resize(nr);
   uint32_t k = 0;
-  for (uint32_t i = 0; i < n; i++)
-    if (!(known && known[i])) c->perm[k++] = i;
-  for (uint32_t i = 0, r = k; i < n; i++)
-    if (known && known[i]) c->perm[r++] = i;
+  for (uint32_t t = 0; t < nr; t++)
+    if (!(known && known[chunk_of(t)])) c->perm[k++] = chunk_of(t);
+  for (uint32_t t = 0, r = k; t < nr; t++)
+    if (known && known[chunk_of(t)]) c->perm[r++] = chunk_of(t);
+  auto size_of = [&](uint32_t i) { return offs[i + 1] - offs[i]; };
+  // waves per SIMD and issue priority of this call's launches (commit_refs' two chunk sets on
+  // two contexts: one wave per SIMD and no priority for the short set, so the long set's
+  // launches always find room and issue first)
+  auto waves_for = [&](uint64_t longest, uint64_t sum) {
+    const int w = hash_waves(longest, sum, c->num_cus);
+    return c->cr_wave_cap > 0 && w > c->cr_wave_cap ? c->cr_wave_cap : w;
+  };
   // With every content hash known (pfscdc_commit_refs), a split Ref.Id pass runs on two
   // streams: the chunks longer than half the longest first on the ctx stream (their ChaCha20
   // pass is short, so the serial BLAKE2b chains that bound the pass start right away), the
@@ -1236,48 +1465,47 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   // smaller one leaves rest chains that outlast the longest one (they run at two waves per
   // SIMD, slower than a lone chain).
   uint32_t nl = 0;
-  if (k == 0 && n > 1 && refid_twostream()) {
-    std::vector<uint64_t> z(n);
+  if (k == 0 && nr > 1 && refid_twostream()) {
     uint64_t longest = 0;
-    for (uint32_t i = 0; i < n; i++) longest = std::max(longest, z[i] = offs[i + 1] - offs[i]);
+    for (uint32_t t = 0; t < nr; t++) longest = std::max(longest, size_of(chunk_of(t)));
     const uint64_t thr = longest * refid_long_pct() / 100;
-    auto is_long = [&](uint32_t i) { return z[i] > thr; };
+    auto is_long = [&](uint32_t i) { return size_of(i) > thr; };
     std::stable_partition(c->perm.begin(), c->perm.end(), is_long);
-    for (uint32_t i = 0; i < n; i++) nl += is_long(i) ? 1 : 0;
-    if (nl == n) nl = 0;
+    for (uint32_t t = 0; t < nr; t++) nl += is_long(chunk_of(t)) ? 1 : 0;
+    if (nl == nr) nl = 0;
   }
   HIP_OK(c, c->h_offs.ensure(n + 1));
   std::memcpy(c->h_offs.p, offs, sizeof(uint64_t) * (n + 1));
-  HIP_OK(c, c->h_segs.ensure(n));
-  for (uint32_t r = 0; r < n; r++) {
+  HIP_OK(c, c->h_segs.ensure(nr));
+  for (uint32_t r = 0; r < nr; r++) {
     const uint32_t i = c->perm[r];
     pfscdc_segment& sg = c->h_segs.p[r];
     std::memset(&sg, 0, sizeof sg);
-    sg.size = offs[i + 1] - offs[i];
+    sg.size = size_of(i);
     sg.file = i;
     sg.flags = PFSCDC_SEG_VALID;
     if (r >= k) std::memcpy(sg.hash, hashes + 32ull * i, 32);
   }
   HIP_OK(c, c->d_offs.ensure(n + 1));
-  HIP_OK(c, c->d_segs.ensure(n));
-  HIP_OK(c, c->d_refs.ensure(n));
-  HIP_OK(c, c->d_order.ensure(n));
+  HIP_OK(c, c->d_segs.ensure(nr));
+  HIP_OK(c, c->d_refs.ensure(nr));
+  HIP_OK(c, c->d_order.ensure(nr));
   HIP_OK(c, c->d_qctr.ensure(3));
   HIP_OK(c, c->d_counts.ensure(6));
-  HIP_OK(c, c->h_refs.ensure(n));
+  HIP_OK(c, c->h_refs.ensure(nr));
   HIP_OK(c, c->h_seg_begin.ensure(4));
   c->h_seg_begin.p[0] = k;  // pinned sources of the device record counts
-  c->h_seg_begin.p[1] = n;
+  c->h_seg_begin.p[1] = nr;
   c->h_seg_begin.p[2] = nl;
-  c->h_seg_begin.p[3] = n - nl;
+  c->h_seg_begin.p[3] = nr - nl;
   HIP_OK(c, hipMemcpyAsync(c->d_offs.p, c->h_offs.p, sizeof(uint64_t) * (n + 1),
                            hipMemcpyHostToDevice, st));
-  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * n,
+  HIP_OK(c, hipMemcpyAsync(c->d_segs.p, c->h_segs.p, sizeof(pfscdc_segment) * nr,
                            hipMemcpyHostToDevice, st));
   HIP_OK(c, hipMemcpyAsync(c->d_counts.p + 1, c->h_seg_begin.p, 4 * sizeof(uint64_t),
                            hipMemcpyHostToDevice, st));
   uint64_t longest_k = 0, sum_k = 0, longest_n = 0, sum_n = 0;
-  for (uint32_t r = 0; r < n; r++) {
+  for (uint32_t r = 0; r < nr; r++) {
     const uint64_t z = c->h_segs.p[r].size;
     if (r < k) {
       longest_k = std::max(longest_k, z);
@@ -1290,14 +1518,14 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   if (k)
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, k, c->d_order.p,
                              c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
-                             hash_waves(longest_k, sum_k, c->num_cus)));
+                             waves_for(longest_k, sum_k), c->cr_hash_prio));
   HIP_OK(c, hipEventRecord(c->cev, st));
   // Ref.Id = Hash(ChaCha20_dek(chunk)).  Fused (the quad computes each block's keystream on
   // its BLAKE2b chain) when the chunks fill the GPU; split into a parallel ChaCha20 pass and
   // a plain BLAKE2b pass over the ciphertext when they do not, so the serial chain of the
   // longest chunk carries only BLAKE2b (about half the per-block latency).
   uint8_t* ct = ctext_out;
-  bool split = refid_split(n, c->num_cus);
+  bool split = refid_split(nr, c->num_cus);
   if (split && !ct) {
     // a ciphertext copy of the whole input, only with room to spare (the fused pass needs
     // none, and other contexts on the device need theirs)
@@ -1312,11 +1540,11 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
       split = false;
   }
   if (split) {
-    // 64-B block prefix per record subset: [0, nl) from h_blk[0], [nl, n) from h_blk[nl + 1]
-    HIP_OK(c, c->h_blk.ensure(n + 2));
-    HIP_OK(c, c->d_blk.ensure(n + 2));
-    HIP_OK(c, c->d_segs2.ensure(n));
-    HIP_OK(c, c->h_segs2.ensure(n));
+    // 64-B block prefix per record subset: [0, nl) from h_blk[0], [nl, nr) from h_blk[nl + 1]
+    HIP_OK(c, c->h_blk.ensure(nr + 2));
+    HIP_OK(c, c->d_blk.ensure(nr + 2));
+    HIP_OK(c, c->d_segs2.ensure(nr));
+    HIP_OK(c, c->h_segs2.ensure(nr));
     uint64_t longest_a = 0, sum_a = 0, longest_b = 0, sum_b = 0;
     c->h_blk.p[0] = 0;
     for (uint32_t r = 0; r < nl; r++) {
@@ -1326,20 +1554,21 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
       sum_a += z;
     }
     c->h_blk.p[nl + 1] = 0;
-    for (uint32_t r = nl; r < n; r++) {
+    for (uint32_t r = nl; r < nr; r++) {
       const uint64_t z = c->h_segs.p[r].size;
       c->h_blk.p[r + 2] = c->h_blk.p[r + 1] + (z + 63) / 64;
       longest_b = std::max(longest_b, z);
       sum_b += z;
     }
-    HIP_OK(c, hipMemcpyAsync(c->d_blk.p, c->h_blk.p, sizeof(uint64_t) * (n + 2),
+    HIP_OK(c, hipMemcpyAsync(c->d_blk.p, c->h_blk.p, sizeof(uint64_t) * (nr + 2),
                              hipMemcpyHostToDevice, st));
-    HIP_OK(c, launch_deks(c->d_segs.p, c->d_counts.p + 2, n, c->d_refs.p, c->d_qctr.p + 1, st));
+    HIP_OK(c, launch_deks(c->d_segs.p, c->d_counts.p + 2, nr, c->d_refs.p, c->d_qctr.p + 1, st));
     // subset [r0, r0 + m) on stream s: ChaCha20 into ct, then BLAKE2b of the ciphertext
     // (pb: where the subset's block prefix starts in h_blk / d_blk)
     auto chacha_pass = [&](uint32_t r0, uint32_t m, uint32_t pb, hipStream_t s) {
       return launch_chacha_xor(data, c->d_offs.p, c->d_segs.p + r0, c->d_blk.p + pb, m,
-                               c->h_blk.p[pb + m], c->d_refs.p + r0, ct, c->num_cus, s);
+                               c->h_blk.p[pb + m], c->d_refs.p + r0, ct, c->num_cus, s,
+                               c->cr_chacha_prio, c->cr_wave_cap > 0);
     };
     auto refid_pass = [&](uint32_t r0, uint32_t m, uint32_t pb, const uint64_t* d_count,
                           uint32_t* ctr, uint64_t longest, uint64_t sum, hipStream_t s,
@@ -1350,8 +1579,8 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
                            hipMemcpyDeviceToDevice, s);
       if (e == hipSuccess)
         e = launch_blake2b(ct, c->d_offs.p, c->d_segs2.p + r0, d_count, m, c->d_order.p + r0,
-                           ctr, c->num_cus, nbytes, s, false, nullptr,
-                           hash_waves(longest, sum, c->num_cus), prio);
+                           ctr, c->num_cus, nbytes, s, false, nullptr, waves_for(longest, sum),
+                           c->cr_hash_prio ? c->cr_hash_prio : prio);
       return e;
     };
     if (nl) {
@@ -1368,39 +1597,55 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
       HIP_OK(c, hipStreamWaitEvent(c->aux_stream, c->xev[0], 0));
       HIP_OK(c, refid_pass(0, nl, 0, c->d_counts.p + 3, c->d_qctr.p + 1, longest_a, sum_a, st,
                            1u, false));
-      HIP_OK(c, refid_pass(nl, n - nl, nl + 1, c->d_counts.p + 4, c->d_qctr.p + 2, longest_b,
+      HIP_OK(c, refid_pass(nl, nr - nl, nl + 1, c->d_counts.p + 4, c->d_qctr.p + 2, longest_b,
                            sum_b, c->aux_stream, 0u, true));
       HIP_OK(c, hipEventRecord(c->xev[1], c->aux_stream));
       HIP_OK(c, hipStreamWaitEvent(st, c->xev[1], 0));
     } else {
-      HIP_OK(c, refid_pass(0, n, 1, c->d_counts.p + 2, c->d_qctr.p + 1, longest_n, sum_n, st,
+      HIP_OK(c, refid_pass(0, nr, 1, c->d_counts.p + 2, c->d_qctr.p + 1, longest_n, sum_n, st,
                            0u, true));
     }
   } else {
     HIP_OK(c, launch_order(c->d_segs.p, c->d_counts.p + 2, c->d_order.p, c->d_qctr.p + 1, st));
-    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, n, c->d_order.p,
+    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 2, nr, c->d_order.p,
                              c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p, ctext_out, st,
-                             hash_waves(longest_n, sum_n, c->num_cus)));
+                             waves_for(longest_n, sum_n), c->cr_hash_prio));
   }
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   if (hashes && k)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * k,
                              hipMemcpyDeviceToHost, st));
-  HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, sizeof(pfscdc_ref) * n,
+  HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, sizeof(pfscdc_ref) * nr,
                            hipMemcpyDeviceToHost, st));
   if (split)
-    HIP_OK(c, hipMemcpyAsync(c->h_segs2.p, c->d_segs2.p, sizeof(pfscdc_segment) * n,
+    HIP_OK(c, hipMemcpyAsync(c->h_segs2.p, c->d_segs2.p, sizeof(pfscdc_segment) * nr,
                              hipMemcpyDeviceToHost, st));
-  HIP_OK(c, hipStreamSynchronize(st));
-  for (uint32_t r = 0; r < n; r++) {
-    const uint32_t i = c->perm[r];
-    refs[i] = c->h_refs.p[r];
-    if (split) std::memcpy(refs[i].id, c->h_segs2.p[r].hash, 32);
-    if (hashes && r < k) std::memcpy(hashes + 32ull * i, c->h_segs.p[r].hash, 32);
-  }
-  c->nsegs = 0;  // the scan results were overwritten
+  c->cr.active = true;
+  c->cr.split = split;
+  c->cr.k = k;
+  c->cr.nr = nr;
+  c->cr.hashes = hashes;
+  c->cr.refs = refs;
+  c->nsegs = 0;  // the scan results are being overwritten
   c->have_refs = false;
   c->scan_valid = false;
+  return finish ? create_refs_finish(c) : PFSCDC_OK;
+}
+
+// The second half of create_refs_device(finish = false): wait for the ctx stream, then the
+// refs (and computed content hashes) of every record into the caller's arrays.
+int create_refs_finish(pfscdc_ctx* c) {
+  if (!c->cr.active) return PFSCDC_OK;
+  const CreatePending p = c->cr;
+  c->cr = CreatePending{};
+  HIP_OK(c, hipSetDevice(c->device));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t r = 0; r < p.nr; r++) {
+    const uint32_t i = c->perm[r];
+    p.refs[i] = c->h_refs.p[r];
+    if (p.split) std::memcpy(p.refs[i].id, c->h_segs2.p[r].hash, 32);
+    if (p.hashes && r < p.k) std::memcpy(p.hashes + 32ull * i, c->h_segs.p[r].hash, 32);
+  }
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, c->ev[7], c->ev[6]) == hipSuccess) c->create_ms = ms;
   if (hipEventElapsedTime(&ms, c->ev[7], c->cev) == hipSuccess) c->create_hash_ms = ms;

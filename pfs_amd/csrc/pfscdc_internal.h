@@ -66,9 +66,13 @@ int scan_sync(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_
 // bytes; offs absolute, offs[0] may be > 0).  hashes (32 B per chunk, may be NULL): in where
 // known[i], else out (Hash(chunk)).  refs: out.  Synchronous.
 // ctext_out (device, nullable): the ciphertexts at the same offsets as data.
+// sel (nullable): only chunks sel[0..nsel).  finish = false: enqueue only, then
+// create_refs_finish(ctx) waits and writes hashes / refs.
 int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
                        const uint64_t* offs, uint32_t n, uint8_t* hashes, const uint8_t* known,
-                       pfscdc_ref* refs, uint8_t* ctext_out = nullptr);
+                       pfscdc_ref* refs, uint8_t* ctext_out = nullptr,
+                       const uint32_t* sel = nullptr, uint32_t nsel = 0, bool finish = true);
+int create_refs_finish(pfscdc_ctx* ctx);
 int ctx_device(const pfscdc_ctx* ctx);
 // grow-only device staging owned by the ctx (writers_close_group): bytes, and the
 // ciphertexts when ctext; both stay valid until the next call or pfscdc_ctx_destroy
@@ -127,14 +131,15 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st, int waves = 0);
+                          uint8_t* ctext_out, hipStream_t st, int waves = 0, uint32_t prio = 0);
 // dek per record (refs[].dek from segs[].hash); zeroes *counter
 hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
                        pfscdc_ref* refs, uint32_t* counter, hipStream_t st);
 // out[range of record r] = ChaCha20_{refs[r].dek}(data[range]); blk_base: prefix of 64-B blocks
 hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pfscdc_segment* segs,
                              const uint64_t* blk_base, uint32_t n, uint64_t nblocks,
-                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st);
+                             const pfscdc_ref* refs, uint8_t* out, int num_cus, hipStream_t st,
+                             bool prio = false, bool one_wave_per_simd = false);
 hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment* segs,
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
                       int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st,

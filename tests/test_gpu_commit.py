@@ -164,3 +164,51 @@ def test_ciphertext_in_place_needs_device_bytes():
     with pytest.raises(_lib.PfsCdcError, match="device bytes"):
         c.commit_refs(data, coffs, known)
     c.close()
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, monkeypatch):
+    """The two-set commit (the long chunks' hashes and chunk.Create on the ctx stream at issue
+    priority, the rest on a helper context beside them, PFSCDC_COMMIT_TWO_SETS) gives the same
+    DataRef hashes, content hashes, Refs and ciphertext as the one-pass form, at several
+    split points (PFSCDC_COMMIT_LONG_PCT), and the oracle's Ref.Id on a sample."""
+    import torch
+
+    p = Ch.Params(average_bits=13, seed=1, min=4000, max=60000)
+    rng = np.random.default_rng(11)
+    lens = np.concatenate([rng.integers(0, 9000, 250), [0, 0, 60000, 60001, 1],
+                           rng.integers(20_000, 250_000, 40)])
+    rng.shuffle(lens)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    host = synthetic_bytes(offs, 91)
+    nf = len(lens)
+    streams = [0, nf // 4, nf // 2, nf]
+    cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+
+    def run(two_sets, pct):
+        monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "1" if two_sets else "0")
+        monkeypatch.setenv("PFSCDC_COMMIT_LONG_PCT", str(pct))
+        c = Chunker(cp, 0)
+        c.set_cuts_only(True)
+        c.set_ctext_in_place(in_place)
+        t = torch.from_numpy(host).to("cuda:0")
+        c.scan(t, offs)
+        coffs, _, known = c.form_chunks(streams)
+        refs, chash, seg = c.commit_refs(t, coffs, known)
+        c.close()
+        return coffs, known, refs, chash, seg, t.cpu().numpy()
+
+    base = run(False, 50)
+    coffs, known, refs0, chash0, seg0, buf0 = base
+    sizes = np.diff(coffs)
+    assert (~known.astype(bool)).sum() > 10 and (sizes > 0.5 * sizes.max()).sum() > 1
+    for pct in (10, 50, 90):
+        _, _, refs, chash, seg, buf = run(True, pct)
+        assert np.array_equal(seg, seg0), pct
+        assert np.array_equal(chash, chash0), pct
+        assert np.array_equal(refs["id"], refs0["id"]) and np.array_equal(refs["dek"], refs0["dek"]), pct
+        assert np.array_equal(buf, buf0), pct  # the plaintext left alone, or the same ciphertext
+    for i in np.linspace(0, len(coffs) - 2, 8).astype(int):
+        chunk = host[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        rid, dek = Ch.create_ref_id(chunk)
+        assert bytes(refs0[i]["id"]) == rid and bytes(refs0[i]["dek"]) == dek
