@@ -706,15 +706,44 @@ PFS_DEV uint32_t lpt_key(uint64_t size) {
   return 1023u - (uint32_t)(k < 1023 ? k : 1023);  // ascending key = descending length
 }
 
+// Hash bins (bin_bytes > 0, next != nullptr): every file of at most bin_bytes is one queue
+// entry, its segments hashed back to back by the quad that takes it (next[i] = the file's
+// following segment, kNoNext after its last); a larger file's segments are entries of their
+// own.  bin_bytes is the launch's bytes per quad, so on many equal files (configs[1]'s
+// aggregated steps: 4 MiB files, 4 MiB per quad) every quad gets the same work and the launch
+// drains with no quad-level imbalance; where segments outweigh a quad's share nothing changes.
+// qlen (nullable): the number of queue entries.
 template <int BLOCK>
 PFS_DEV void lpt_order_block(const pfscdc_segment* __restrict__ segs, uint64_t n,
                              uint32_t* __restrict__ order, uint32_t* __restrict__ counter,
-                             uint32_t* hist, uint64_t* s_wave) {
+                             uint32_t* hist, uint64_t* s_wave,
+                             const uint64_t* __restrict__ offs = nullptr, uint64_t bin_bytes = 0,
+                             uint32_t* __restrict__ next = nullptr, uint64_t* qlen = nullptr) {
+  const bool bins = next && offs && bin_bytes;
+  auto binned = [&](uint64_t i) {
+    const uint32_t f = segs[i].file;
+    return bins && offs[f + 1] - offs[f] <= bin_bytes;
+  };
+  // is segment i a queue entry (a bin's first segment, or a segment alone); its sort key
+  auto entry = [&](uint64_t i, uint32_t& key) {
+    if (binned(i)) {
+      const uint32_t f = segs[i].file;
+      key = lpt_key(offs[f + 1] - offs[f]);
+      return i == 0 || segs[i - 1].file != f;
+    }
+    key = lpt_key(segs[i].size);
+    return true;
+  };
   constexpr int kPer = 1024 / BLOCK;  // histogram bins per thread
   static_assert(1024 % BLOCK == 0, "bins split evenly over the block");
   for (int b = 0; b < kPer; b++) hist[threadIdx.x * kPer + b] = 0;
   __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&hist[lpt_key(segs[i].size)], 1u);
+  for (uint64_t i = threadIdx.x; i < n; i += BLOCK) {
+    uint32_t key;
+    if (entry(i, key)) atomicAdd(&hist[key], 1u);
+    if (bins) next[i] = binned(i) && i + 1 < n && segs[i + 1].file == segs[i].file
+                            ? (uint32_t)(i + 1) : kNoNext;
+  }
   __syncthreads();
   uint32_t local[kPer];
   uint64_t sum = 0;
@@ -729,9 +758,14 @@ PFS_DEV void lpt_order_block(const pfscdc_segment* __restrict__ segs, uint64_t n
     start += local[b];
   }
   __syncthreads();
-  for (uint64_t i = threadIdx.x; i < n; i += BLOCK)
-    order[atomicAdd(&hist[lpt_key(segs[i].size)], 1u)] = (uint32_t)i;
-  if (threadIdx.x == 0) *counter = 0;
+  for (uint64_t i = threadIdx.x; i < n; i += BLOCK) {
+    uint32_t key;
+    if (entry(i, key)) order[atomicAdd(&hist[key], 1u)] = (uint32_t)i;
+  }
+  if (threadIdx.x == 0) {
+    *counter = 0;
+    if (qlen) *qlen = total;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -855,7 +889,8 @@ __global__ __launch_bounds__(kSelectBlock) void select_kernel(
     uint64_t mask, uint64_t min_chunk, uint64_t max_chunk,
     pfscdc_segment* __restrict__ slots, uint64_t* __restrict__ nseg, uint32_t* done_ctr,
     pfscdc_segment* __restrict__ segs, uint64_t* __restrict__ seg_begin,
-    uint32_t* __restrict__ order, uint32_t* __restrict__ counter) {
+    uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t bin_bytes,
+    uint32_t* __restrict__ next, uint64_t* __restrict__ qlen) {
   __shared__ uint32_t hist[1024];
   __shared__ uint64_t s_wave[kSelectBlock / 64 + 1];
   __shared__ uint32_t s_flag;
@@ -868,7 +903,9 @@ __global__ __launch_bounds__(kSelectBlock) void select_kernel(
                                                         seg_begin, s_wave);
   __threadfence_block();
   __syncthreads();
-  if (order) lpt_order_block<kSelectBlock>(segs, total, order, counter, hist, s_wave);
+  if (order)
+    lpt_order_block<kSelectBlock>(segs, total, order, counter, hist, s_wave, offs, bin_bytes,
+                                  next, qlen);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1227,7 +1264,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
     pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks,
-    uint64_t* span) {
+    uint64_t* span, const uint32_t* __restrict__ next) {
   constexpr bool CIPHER = MODE != kModeHash;
   const SpanClock span_clk = span_begin(span);
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
@@ -1276,6 +1313,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     prio_blocks = (prio_blocks & 0xc0000000u) |
                   (nseg > (uint64_t)gridDim.x * (kHashBlock / 4) ? 8192u : 0u);
   bool active = false;   // this quad holds a segment
+  uint32_t bin_next = kNoNext;  // hash bins: the quad's next segment (its file's following one)
   bool drained = false;  // wave-uniform: the queue is exhausted
   // wave-uniform: blocks to come in which no quad can finish and the priority cannot change,
   // so the refill ballot, the exit test and the priority ballot are skipped (they cost ~20
@@ -1418,6 +1456,30 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       quiet--;
       fast = quiet >= 3;
     } else {
+      auto begin = [&](uint32_t s) {  // start segment s on this quad
+        sidx = s;
+        seg = segs + sidx;
+        L = seg->size;
+        if (CIPHER) {
+          const uint32_t* dk = reinterpret_cast<const uint32_t*>(refs[sidx].dek);
+          key_b = dk[j];
+          key_c = dk[4 + j];
+        }
+        src = data + offs[seg->file] + seg->offset;
+        if (MODE != kModeHash && out) dst_base = out + offs[seg->file] + seg->offset;
+        nblk = L == 0 ? 1 : (L + 127) / 128;
+        blk = 0;
+        ha = h0a;
+        hb = h0b;
+        active = true;
+        load_block(0);
+        lds_put(cur);
+        if (nblk > 1) load_block(1);
+      };
+      if (!active && bin_next != kNoNext) {  // the rest of the quad's bin, no queue access
+        begin(bin_next);
+        bin_next = kNoNext;
+      }
       if (!drained) {
         const bool need = !active;
         const uint64_t want = __ballot(need && j == 0);  // one bit per idle quad (its lane 0)
@@ -1430,26 +1492,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
           if (need) {
             const uint64_t below = want & ((1ULL << (lane & ~3u)) - 1);
             const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(below);
-            if (idx < nseg) {
-              sidx = order[idx];
-              seg = segs + sidx;
-              L = seg->size;
-              if (CIPHER) {
-                const uint32_t* dk = reinterpret_cast<const uint32_t*>(refs[sidx].dek);
-                key_b = dk[j];
-                key_c = dk[4 + j];
-              }
-              src = data + offs[seg->file] + seg->offset;
-              if (MODE != kModeHash && out) dst_base = out + offs[seg->file] + seg->offset;
-              nblk = L == 0 ? 1 : (L + 127) / 128;
-              blk = 0;
-              ha = h0a;
-              hb = h0b;
-              active = true;
-              load_block(0);
-              lds_put(cur);
-              if (nblk > 1) load_block(1);
-            }
+            if (idx < nseg) begin(order[idx]);
           }
           if ((uint64_t)base + cnt >= nseg) drained = true;
         }
@@ -1550,6 +1593,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         if (MODE == kModeRefId) reinterpret_cast<uint64_t*>(refs[sidx].id)[j] = ha;
         else reinterpret_cast<uint64_t*>(seg->hash)[j] = ha;
         active = false;
+        if (next) bin_next = next[sidx];
       }
     }
     return true;
@@ -1981,7 +2025,7 @@ hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uin
                          uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
                          uint64_t* nseg, uint32_t* done_ctr, pfscdc_segment* segs,
                          uint64_t* seg_begin, uint32_t* order, uint32_t* counter,
-                         hipStream_t st) {
+                         hipStream_t st, uint64_t bin_bytes, uint32_t* next, uint64_t* qlen) {
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   const uint64_t waves_per_block = kSelectBlock / 64;
   const uint64_t grid = (nfiles + waves_per_block - 1) / waves_per_block;
@@ -1989,7 +2033,7 @@ hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uin
                                                          offs, seg_base, nfiles, mask64,
                                                          min_chunk, max_chunk, slots, nseg,
                                                          done_ctr, segs, seg_begin, order,
-                                                         counter);
+                                                         counter, bin_bytes, next, qlen);
   return hipGetLastError();
 }
 
@@ -2051,7 +2095,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered, uint64_t* span, int waves, uint32_t prio,
-                          bool cu_exclusive) {
+                          bool cu_exclusive, const uint32_t* next) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   if (kHashLanesPerSegment == 1) {
@@ -2071,7 +2115,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const size_t dyn = cu_exclusive ? 64u * 1024u : 0u;
   blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, dyn, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
-      prio ? prio : hash_prio_blocks(), span);
+      prio ? prio : hash_prio_blocks(), span, ordered ? next : nullptr);
   return hipGetLastError();
 }
 
@@ -2084,12 +2128,13 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st, int waves, uint32_t prio) {
+                          uint8_t* ctext_out, hipStream_t st, int waves, uint32_t prio,
+                          const uint32_t* next) {
   if (max_segments == 0) return hipSuccess;
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
-      prio ? prio : hash_prio_blocks(), nullptr);
+      prio ? prio : hash_prio_blocks(), nullptr, next);
   return hipGetLastError();
 }
 
@@ -2122,7 +2167,7 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   blake2b_kernel<kModeGet><<<hash_grid(nsegs, num_cus, waves), kHashBlock, 0, st>>>(
       ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
-      nullptr);
+      nullptr, nullptr);
   return hipGetLastError();
 }
 

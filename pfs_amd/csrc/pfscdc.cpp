@@ -95,6 +95,7 @@ struct pfscdc_ctx {
   DevBuf<uint64_t> d_offs, d_seg_base, d_nseg, d_seg_begin;
   DevBuf<pfscdc_segment> d_slots, d_segs;
   DevBuf<uint32_t> d_order, d_qctr;  // LPT segment order + hash queue counter
+  DevBuf<uint32_t> d_next;            // hash bins: each segment's successor in its bin
   DevBuf<pfscdc_ref> d_refs;
   DevBuf<uint8_t> d_out;  // get_chunks: plaintext when the caller's output is on the host
   // kernel execution spans: [0,1] scan begin/end, [2,3] hash begin/end; shader-clock sums
@@ -126,6 +127,7 @@ struct pfscdc_ctx {
   int cr_wave_cap = 0;
   uint32_t cr_hash_prio = 0;
   bool cr_chacha_prio = false;
+  bool cr_one_stream = false;  // no second-stream split of the Ref.Id pass
   pfscdc_ctx* helper = nullptr;  // commit_refs: the short chunk set's context (lazy)
   hipEvent_t pev[3] = {nullptr, nullptr, nullptr};  // commit_refs: start, long / short unions
   bool have_refs = false;
@@ -148,6 +150,15 @@ const pfscdc_params& ctx_params(const pfscdc_ctx* ctx) { return ctx->params; }
 }  // namespace pfscdc
 
 namespace {
+
+// PFSCDC_HASH_BINS=0: no hash bins (every segment its own queue entry; A/B)
+bool hash_bins_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_HASH_BINS");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 
 // PFSCDC_HASH_CU_EXCLUSIVE=0: chain-bound scan hashes may share CUs with another launch (A/B)
 bool hash_cu_exclusive() {
@@ -236,6 +247,16 @@ int pfscdc_go_int63(int64_t seed, int64_t* out, int n) {
 }
 
 int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out) {
+  return pfscdc::ctx_create_on(params, device, nullptr, out);
+}
+
+}  // extern "C"
+
+// A context on the caller's stream (shared != nullptr: no stream of its own; commit_refs'
+// helper runs on its owner's second stream, so the commit uses two hardware queues, not
+// four: streams beyond GPU_MAX_HW_QUEUES share a queue and serialize).
+int pfscdc::ctx_create_on(const pfscdc_params* params, int device, hipStream_t shared,
+                          pfscdc_ctx** out) {
   if (!out) return PFSCDC_EINVAL;
   *out = nullptr;
   std::string why;
@@ -268,7 +289,7 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
     return PFSCDC_EHIP;
   }
   generate_hashes(params->seed, c->table);
-  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+  if ((!shared && hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) ||
       hipMalloc((void**)&c->d_table, sizeof c->table) != hipSuccess ||
       hipMemcpy(c->d_table, c->table, sizeof c->table, hipMemcpyHostToDevice) != hipSuccess) {
     delete c;
@@ -284,15 +305,18 @@ int pfscdc_ctx_create(const pfscdc_params* params, int device, pfscdc_ctx** out)
     delete c;
     return PFSCDC_EHIP;
   }
-  c->stream = c->own_stream;
+  c->stream = shared ? shared : c->own_stream;
   *out = c;
   return PFSCDC_OK;
 }
+
+extern "C" {
 
 int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   if (!c) return PFSCDC_EINVAL;
   (void)hipSetDevice(c->device);
   if (c->pending) (void)hipStreamSynchronize(c->stream);
+  if (c->helper) pfscdc_ctx_destroy(c->helper);  // it runs on c->aux_stream
   c->d_data.release();
   c->d_tail.release();
   c->d_recs.release();
@@ -306,6 +330,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_seg_begin.release();
   c->d_slots.release();
   c->d_segs.release();
+  c->d_next.release();
   c->d_order.release();
   c->d_qctr.release();
   c->d_refs.release();
@@ -335,7 +360,6 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   for (auto& e : c->pev)
     if (e) (void)hipEventDestroy(e);
-  if (c->helper) pfscdc_ctx_destroy(c->helper);
   for (auto& e : c->xev)
     if (e) (void)hipEventDestroy(e);
   delete c;
@@ -408,6 +432,12 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   // the hash's longest chain is at most the largest file and at most max_chunk
   const int waves = hash_waves(std::min<uint64_t>(longest_file, (uint64_t)p.max_chunk), nbytes,
                                c->num_cus);
+  // hash bins: the files of at most one quad's share of the bytes are hashed whole by one
+  // quad each (lpt_order_block); PFSCDC_HASH_BINS=0: every segment its own queue entry (A/B)
+  const uint64_t quads = (uint64_t)c->num_cus * 4 * (uint64_t)waves * 16;
+  uint64_t bin_bytes = hash_bins_enabled() ? (nbytes + quads - 1) / quads : 0;
+  if (const char* e = getenv("PFSCDC_HASH_BIN_BYTES"))  // a fixed bin size (tests, A/B)
+    bin_bytes = strtoull(e, nullptr, 10);
   c->h_seg_base.p[nfiles] = cap;
   c->slot_cap = cap;
   c->nfiles = nfiles;
@@ -420,12 +450,13 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_slots.ensure(cap));
   HIP_OK(c, c->d_segs.ensure(cap));
   HIP_OK(c, c->d_order.ensure(cap));
+  if (bin_bytes) HIP_OK(c, c->d_next.ensure(cap));
   HIP_OK(c, c->d_qctr.ensure(2));
   if (options & PFSCDC_OPT_REF_IDS) HIP_OK(c, c->d_refs.ensure(cap));
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_unit_ctr.ensure(3));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
-  HIP_OK(c, c->d_counts.ensure(4));
+  HIP_OK(c, c->d_counts.ensure(5));  // [4]: the hash queue's length (select)
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
   HIP_OK(c, c->d_span.ensure(kSpanSlots));
   HIP_OK(c, c->h_span.ensure(kSpanSlots + 1));
@@ -449,7 +480,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nbytes > n_main)
     HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main,
                              hipMemcpyDeviceToDevice, st));
-  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 4 * sizeof(uint64_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 5 * sizeof(uint64_t), st));
   // the scan adds candidates to the tile records with atomics
   if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
   HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));  // + done counters
@@ -478,7 +509,11 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                             c->d_seg_base.p, nfiles, p.average_bits, (uint64_t)p.min_chunk,
                             (uint64_t)p.max_chunk, c->d_slots.p, c->d_nseg.p,
                             c->d_unit_ctr.p + 2, c->d_segs.p, c->d_seg_begin.p, c->d_order.p,
-                            c->d_qctr.p, st));
+                            c->d_qctr.p, st, bin_bytes, bin_bytes ? c->d_next.p : nullptr,
+                            c->d_counts.p + 4));
+  // the queue: its length from the selection (bins count once), the bins' successor links
+  const uint64_t* qlen = c->d_counts.p + 4;
+  const uint32_t* next = bin_bytes ? c->d_next.p : nullptr;
   HIP_OK(c, hipEventRecord(c->ev[3], st));
   // steps in flight on several ctxs: this step's hash starts after the other ctx's last
   // enqueued hash (the scans still overlap the hash tails; two hashes never share the CUs)
@@ -491,16 +526,16 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     HIP_OK(c, set_wave_trace(c->d_wtrace.p, st));
   }
   if (nfiles && !(options & kScanNoHash))
-    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
+    HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
-                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive()));
+                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive(), next));
   if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
-    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, c->d_seg_begin.p + nfiles, cap,
+    HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p,
-                             nullptr, st, waves));
+                             nullptr, st, waves, 0u, next));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)
@@ -795,6 +830,12 @@ static uint64_t commit_long_pct() {
   return (uint64_t)(x > 0 && x < 100 ? x : 50);
 }
 
+static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
+  const char* e = getenv("PFSCDC_COMMIT_SHORT_WAVES");
+  const int x = e ? atoi(e) : 0;
+  return x >= 1 && x <= 2 ? x : 1;
+}
+
 static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
                                 const std::vector<uint64_t>& sbeg, const std::vector<uint64_t>& ssz,
                                 const uint64_t* co, uint32_t nchunks, uint8_t* content_hashes,
@@ -828,7 +869,11 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     nlong += set_of[i] == 0;
   }
   if (nlong == 0 || nlong == nchunks) return kOnePass;
-  if (!c->helper && pfscdc_ctx_create(&c->params, c->device, &c->helper) != PFSCDC_OK) {
+  if (!c->aux_stream) {
+    HIP_OK(c, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    for (auto& e : c->xev) HIP_OK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  if (!c->helper && ctx_create_on(&c->params, c->device, c->aux_stream, &c->helper) != PFSCDC_OK) {
     c->helper = nullptr;
     return kOnePass;
   }
@@ -887,7 +932,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     if (R)
       HIP_OK(c, launch_blake2b(data, u->d_offs.p, u->d_segs.p, u->d_counts.p + 1, R, u->d_order.p,
                                u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
-                               x ? 1 : w, x ? kNoPrio : 1u));
+                               x ? std::min(w, commit_short_waves()) : w, x ? kNoPrio : 1u));
     if (R)
       HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
                                hipMemcpyDeviceToHost, st));
@@ -912,14 +957,16 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
       for (uint32_t i : sel[x])
         if (hash_known[i])
           std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * known_seg[i], 32);
-      u->cr_wave_cap = x ? 1 : 0;
+      u->cr_wave_cap = x ? commit_short_waves() : 0;
       u->cr_hash_prio = x ? kNoPrio : 1u;
       u->cr_chacha_prio = x == 0;
+      u->cr_one_stream = true;  // each set has one stream (two in all)
       const int rc = create_refs_device(u, data, nbytes, co, nchunks, content_hashes, all.data(),
                                         refs, ct, sel[x].data(), (uint32_t)sel[x].size(), false);
       u->cr_wave_cap = 0;
       u->cr_hash_prio = 0;
       u->cr_chacha_prio = false;
+      u->cr_one_stream = false;
       if (rc) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamSynchronize(X[1]->stream);
@@ -1465,7 +1512,7 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   // smaller one leaves rest chains that outlast the longest one (they run at two waves per
   // SIMD, slower than a lone chain).
   uint32_t nl = 0;
-  if (k == 0 && nr > 1 && refid_twostream()) {
+  if (k == 0 && nr > 1 && refid_twostream() && !c->cr_one_stream) {
     uint64_t longest = 0;
     for (uint32_t t = 0; t < nr; t++) longest = std::max(longest, size_of(chunk_of(t)));
     const uint64_t thr = longest * refid_long_pct() / 100;

@@ -40,6 +40,7 @@ constexpr int kHashLanesPerSegment = PFS_HASH_LANES;  // 4: blake2b_kernel (prod
 constexpr int kHashLaneBlock = 256;
 constexpr uint64_t kDenseBit = 1ULL << 63;
 constexpr uint64_t kNone = ~0ULL;
+constexpr uint32_t kNoNext = 0xffffffffu;  // hash bins: no following segment
 constexpr uint64_t kTailBytes = 256;  // zero-padded copy of the final partial 64-byte block
 
 struct TileRec {
@@ -73,6 +74,8 @@ int create_refs_device(pfscdc_ctx* ctx, const uint8_t* data, uint64_t nbytes,
                        pfscdc_ref* refs, uint8_t* ctext_out = nullptr,
                        const uint32_t* sel = nullptr, uint32_t nsel = 0, bool finish = true);
 int create_refs_finish(pfscdc_ctx* ctx);
+// pfscdc_ctx_create on a given stream (shared: the ctx creates none and never destroys it)
+int ctx_create_on(const pfscdc_params* params, int device, hipStream_t shared, pfscdc_ctx** out);
 int ctx_device(const pfscdc_ctx* ctx);
 // grow-only device staging owned by the ctx (writers_close_group): bytes, and the
 // ciphertexts when ctext; both stay valid until the next call or pfscdc_ctx_destroy
@@ -114,7 +117,8 @@ hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uin
                          uint64_t min_chunk, uint64_t max_chunk, pfscdc_segment* slots,
                          uint64_t* nseg, uint32_t* done_ctr, pfscdc_segment* segs,
                          uint64_t* seg_begin, uint32_t* order, uint32_t* counter,
-                         hipStream_t st);
+                         hipStream_t st, uint64_t bin_bytes = 0, uint32_t* next = nullptr,
+                         uint64_t* qlen = nullptr);
 hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_base,
                              const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
                              uint64_t* seg_begin, hipStream_t st);
@@ -123,7 +127,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered = false, uint64_t* span = nullptr, int waves = 0,
                           uint32_t prio = 0,  // prio: issue-priority threshold (0: default)
-                          bool cu_exclusive = false);  // one workgroup per CU (see launcher)
+                          bool cu_exclusive = false,  // one workgroup per CU (see launcher)
+                          const uint32_t* next = nullptr);  // hash bins (lpt_order_block)
 // waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all
 int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
@@ -131,7 +136,8 @@ hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, u
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
-                          uint8_t* ctext_out, hipStream_t st, int waves = 0, uint32_t prio = 0);
+                          uint8_t* ctext_out, hipStream_t st, int waves = 0, uint32_t prio = 0,
+                          const uint32_t* next = nullptr);
 // dek per record (refs[].dek from segs[].hash); zeroes *counter
 hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
                        pfscdc_ref* refs, uint32_t* counter, hipStream_t st);

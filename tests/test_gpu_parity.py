@@ -265,3 +265,29 @@ def test_kernel_spans_and_clocks_are_recorded():
     for k in ("scan_mhz", "hash_mhz"):
         assert 400 < tm[k] < 3000, (k, tm[k])
     c.close()
+
+
+@pytest.mark.parametrize("bin_bytes", ["0", "60000", "1000000000000"])
+@pytest.mark.parametrize("ref_ids", [False, True])
+def test_hash_bins_equal_oracle(bin_bytes, ref_ids, monkeypatch):
+    """Hash bins (a quad hashes every segment of a file of at most bin_bytes back to back,
+    lpt_order_block): digests, and with PFSCDC_OPT_REF_IDS the per-segment Ref.Ids, equal to
+    the oracle whether no file, some files or every file forms a bin (empty files and files
+    cut into many segments included)."""
+    monkeypatch.setenv("PFSCDC_HASH_BIN_BYTES", bin_bytes)
+    rng = np.random.default_rng(5)
+    lens = np.concatenate([rng.integers(0, 70_000, 200), [0, 0, 1, 30_000, 250_000, 0]])
+    rng.shuffle(lens)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 23)
+    c = Chunker(cp(SMALL), device=0, ref_ids=ref_ids)
+    res = c.scan(data, offs)
+    assert_same(res, data, offs, SMALL)
+    if ref_ids:
+        refs = res.refs
+        for i in np.linspace(0, len(res.segments) - 1, 10).astype(int):
+            g = res.segments[i]
+            a = int(offs[g["file"]] + g["offset"])
+            rid, dek = Ch.create_ref_id(data[a:a + int(g["size"])].tobytes())
+            assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek
+    c.close()
