@@ -1264,7 +1264,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
     pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks,
-    uint64_t* span, const uint32_t* __restrict__ next) {
+    uint64_t* span, const uint32_t* __restrict__ next, uint64_t* __restrict__ fair) {
   constexpr bool CIPHER = MODE != kModeHash;
   const SpanClock span_clk = span_begin(span);
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
@@ -1429,6 +1429,15 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // of these execute in their own loop, straight-line code between the round blocks.
   // the fast loop's byte counter t (lane 0 only: ((blk + 1) << 7) & t_mask), advanced by one
   // 64-bit add per block instead of rebuilt from blk (shift, add, two selects)
+  // Fair share (fair != nullptr, hash bins): the two waves of a SIMD hold equal work, but the
+  // SIMD's arbiter lets one run ahead (oldest first), which then ends early and leaves the
+  // other alone at the lone-wave rate.  At least every kFairEvery blocks each wave adds the
+  // blocks it ran to a launch-wide counter and raises its issue priority while it is behind
+  // the launch's average, so the waves of a SIMD advance together.
+  constexpr uint32_t kFairEvery = 256;
+  uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; fair share, the trace)
+  uint32_t reported = 0;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kHashBlock / 64);
   uint64_t tm = 0;
   const uint64_t tinc = 128 & t_mask;
   auto fast_step = [&](auto par, uint64_t* pre) {
@@ -1498,7 +1507,16 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         }
       }
       if (__ballot(active) == 0) return false;  // every quad idle and the queue empty
-      if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
+      if (fair) {
+        const uint32_t d = wave_steps - reported;
+        uint64_t tot = 0;
+        if (lane == 0) tot = atomicAdd((unsigned long long*)fair, (unsigned long long)d);
+        tot = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tot >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tot);
+        reported = wave_steps;
+        if ((uint64_t)wave_steps * nwaves < tot + d) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
         const uint64_t T = prio_blocks & 0x3fffffffu, rem = active ? nblk - blk : 0;
         if (prio_blocks & 0x40000000u) {  // graded: 3 above 2T, 2 above T, 1 above T/2
           if (__ballot(rem > 2 * T)) __builtin_amdgcn_s_setprio(3);
@@ -1516,7 +1534,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       const uint64_t rem64 = active ? nblk - blk : 0;
       const uint32_t rem = rem64 > 0xffffffffULL ? 0xffffffffu : (uint32_t)rem64;
       uint32_t q = wave_min_u32(active ? rem : 0xffffffffu) - 1;
-      if (prio_blocks & 0x3fffffffu) {
+      if (fair && q > kFairEvery - 1) q = kFairEvery - 1;
+      if (!fair && (prio_blocks & 0x3fffffffu)) {
         // the next block at which the longest chain left crosses a priority threshold
         const uint32_t T = prio_blocks & 0x3fffffffu, rmax = wave_max_u32(rem);
         const uint32_t th[3] = {graded ? 2 * T : T, T, T / 2};
@@ -1604,7 +1623,6 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // active quad at least Q blocks from its end, so pairs of fast blocks need Q >= 5
   // (one copy of the fast loop, entered after a parity-1 step: one hot loop body in the
   // instruction cache)
-  uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; the development trace)
   while (true) {
     if (!step(P0)) break;
     if (!step(P1)) break;
@@ -2095,7 +2113,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered, uint64_t* span, int waves, uint32_t prio,
-                          bool cu_exclusive, const uint32_t* next) {
+                          bool cu_exclusive, const uint32_t* next, uint64_t* fair) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   if (kHashLanesPerSegment == 1) {
@@ -2115,7 +2133,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const size_t dyn = cu_exclusive ? 64u * 1024u : 0u;
   blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, dyn, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
-      prio ? prio : hash_prio_blocks(), span, ordered ? next : nullptr);
+      prio ? prio : hash_prio_blocks(), span, ordered ? next : nullptr,
+      ordered && next ? fair : nullptr);
   return hipGetLastError();
 }
 
@@ -2134,7 +2153,7 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
-      prio ? prio : hash_prio_blocks(), nullptr, next);
+      prio ? prio : hash_prio_blocks(), nullptr, next, nullptr);
   return hipGetLastError();
 }
 
@@ -2167,7 +2186,7 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   blake2b_kernel<kModeGet><<<hash_grid(nsegs, num_cus, waves), kHashBlock, 0, st>>>(
       ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
-      nullptr, nullptr);
+      nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 

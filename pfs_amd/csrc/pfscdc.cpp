@@ -160,6 +160,15 @@ bool hash_bins_enabled() {
   return on;
 }
 
+// PFSCDC_HASH_FAIR=0: hash bins without the fair-share issue priority (A/B)
+bool hash_fair_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_HASH_FAIR");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // PFSCDC_HASH_CU_EXCLUSIVE=0: chain-bound scan hashes may share CUs with another launch (A/B)
 bool hash_cu_exclusive() {
   static const bool on = [] {
@@ -456,7 +465,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_unit_ctr.ensure(3));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
-  HIP_OK(c, c->d_counts.ensure(5));  // [4]: the hash queue's length (select)
+  HIP_OK(c, c->d_counts.ensure(6));  // [4]: the hash queue's length (select), [5] fair share
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
   HIP_OK(c, c->d_span.ensure(kSpanSlots));
   HIP_OK(c, c->h_span.ensure(kSpanSlots + 1));
@@ -480,7 +489,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nbytes > n_main)
     HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main,
                              hipMemcpyDeviceToDevice, st));
-  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 5 * sizeof(uint64_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 6 * sizeof(uint64_t), st));
   // the scan adds candidates to the tile records with atomics
   if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
   HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));  // + done counters
@@ -528,7 +537,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
-                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive(), next));
+                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive(), next,
+                             hash_fair_enabled() ? c->d_counts.p + 5 : nullptr));
   if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
@@ -810,7 +820,7 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
 // record, then one Ref.Id pass, A/B).  A chunk's Ref.Id needs only its own content hash, and
 // the commit's critical path is the longest chunks' two serial chains (content hash, then the
 // BLAKE2b of its ciphertext, writer.go:240 + client.go:57).  So the chunks longer than
-// PFSCDC_COMMIT_LONG_PCT (default 50) percent of the longest, with every segment inside them,
+// PFSCDC_COMMIT_LONG_PCT (default 30) percent of the longest, with every segment inside them,
 // form the long set on this ctx's stream: their hashes, then at once their deks, ChaCha20 and
 // Ref.Id chains, at issue priority 2.  The rest (segments, content hashes and chunk.Create of
 // the shorter chunks) runs on a helper ctx's stream beside them, at one wave per SIMD so the
@@ -819,15 +829,22 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
 constexpr int kOnePass = 1;
 constexpr uint32_t kNoPrio = 0x40000000u;  // hash launch prio_blocks: never raise priority
 
-// read at every call (tests switch them per call)
-static bool commit_two_sets() {
+// read at every call (tests switch them per call).  PFSCDC_COMMIT_TWO_SETS: 0 off, 1 on,
+// unset auto: on when the commit's chunks outnumber the quads of one wave per SIMD (the
+// chunk chains alone then keep the GPU busy past the longest chunk's two chains: c4 at two
+// commits per step, 28K chunks, 342 -> 362 GiB/s; at one commit, 14K chunks, the one-pass
+// form is faster: 248 vs 230-233 GiB/s, profiles/r3/two_sets/)
+static bool commit_two_sets(uint32_t nchunks, int num_cus) {
   const char* e = getenv("PFSCDC_COMMIT_TWO_SETS");
-  return !(e && atoi(e) == 0);
+  if (e && *e) return atoi(e) != 0;
+  return (uint64_t)nchunks > (uint64_t)num_cus * 4 * 16;
 }
+// the long set: chunks longer than this percentage of the longest (PFSCDC_COMMIT_LONG_PCT;
+// c4 G = 2: 10% 335, 20% 305, 30% 362, 35% 356, 40% 338, 50% 305 GiB/s)
 static uint64_t commit_long_pct() {
   const char* e = getenv("PFSCDC_COMMIT_LONG_PCT");
   const int x = e ? atoi(e) : 0;
-  return (uint64_t)(x > 0 && x < 100 ? x : 50);
+  return (uint64_t)(x > 0 && x < 100 ? x : 30);
 }
 
 static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
@@ -841,7 +858,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
                                 const uint64_t* co, uint32_t nchunks, uint8_t* content_hashes,
                                 const uint8_t* hash_known, pfscdc_ref* refs,
                                 uint8_t* segment_hashes, uint8_t* ct) {
-  if (!commit_two_sets() || nchunks < 2) return kOnePass;
+  if (!commit_two_sets(nchunks, c->num_cus) || nchunks < 2) return kOnePass;
   const uint64_t m = sbeg.size();
   // the chunk holding each segment; the segment a one-segment chunk's content hash is
   std::vector<uint32_t> seg_chunk(m);

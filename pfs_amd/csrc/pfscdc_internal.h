@@ -128,7 +128,8 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           bool ordered = false, uint64_t* span = nullptr, int waves = 0,
                           uint32_t prio = 0,  // prio: issue-priority threshold (0: default)
                           bool cu_exclusive = false,  // one workgroup per CU (see launcher)
-                          const uint32_t* next = nullptr);  // hash bins (lpt_order_block)
+                          const uint32_t* next = nullptr,  // hash bins (lpt_order_block)
+                          uint64_t* fair = nullptr);  // bins: fair-share counter (zeroed)
 // waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all
 int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
