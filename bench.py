@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
                          "one context + host thread each over the step's one input buffer); "
-                         "0 = auto: 2 for --path put on c3 (1 if HBM cannot hold 2 inputs), else 1")
+                         "0 = auto: 4 for --path put on c3 (fewer if HBM cannot hold them), else 1")
     ap.add_argument("--hash-order", default="free", choices=["serial", "free"],
                     help="steps in flight: serial = a step's hash kernel starts after the "
                          "previous step's (scans overlap hash tails; each hash launch has the "
@@ -298,6 +298,11 @@ def med(xs):
 
 def main():
     args = parse()
+    # HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
+    # share a queue and run one after the other: c3's four streams in flight (one context
+    # each) and the commit's two chunk sets need a queue per stream.  Set
+    # before the first HIP call; an explicit setting wins.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -347,11 +352,12 @@ def main():
 
     # One step at a time by default, so every kernel launch has the GPU to itself and its
     # duration (HIP events, in-kernel span and a kernel trace alike) is its own.  c3 (one
-    # stream, bound by its longest 20 MB chains) runs two steps in flight on two contexts;
+    # stream, bound by its longest 20 MB chains: ~175 ms per stream whatever else runs) runs
+    # four steps in flight on four contexts (one hardware queue each, GPU_MAX_HW_QUEUES);
     # c2's two-in-flight throughput is measured after the timed region (``two_in_flight``).
     # c4/c5 hold >= 16K chains per step through --group instead.
     S = args.inflight if args.inflight > 0 else (
-        2 if args.path == "put" and args.config == "c3" else 1)
+        4 if args.path == "put" and args.config == "c3" else 1)
     batches = []
     for k in range(S):
         try:
@@ -545,13 +551,19 @@ def main():
     if S > 1:
         # after the timed region: steps alone on the GPU (median of 3), so the kernels' own
         # durations can be read beside the overlapped ones above
-        iso = []
+        iso, walls = [], []
         for _ in range(3):
+            w0 = time.perf_counter()
             chunkers[0].scan_async(batches[0], work.offs)
             chunkers[0].wait()
+            walls.append((time.perf_counter() - w0) * 1e3)
             iso.append(chunkers[0].timings())
         im = {name: med([s[name] for s in iso]) for name in iso[0]}
         out["kernel_ms_isolated"] = im
+        # one step alone, host to host: the per-stream latency the steps in flight hide
+        out["one_step_alone"] = {"value": round(total / (med(walls) * 1e-3) / GIB, 3),
+                                 "unit": "GiB/s", "ms": med(walls),
+                                 "note": "one step with nothing else in flight (median of 3)"}
         ri = roof(im["hash_span"], "blake2b_kernel")
         rc = roof(im["scan_span"], "cdc_scan_kernel")
         out["roofline_isolated"] = {"hash": ri, "scan": rc,

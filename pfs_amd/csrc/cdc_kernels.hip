@@ -1264,7 +1264,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes,
     pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio_blocks,
-    uint64_t* span, const uint32_t* __restrict__ next, uint64_t* __restrict__ fair) {
+    uint64_t* span, const uint32_t* __restrict__ next, uint64_t* __restrict__ fair,
+    uint32_t fair_every) {
   constexpr bool CIPHER = MODE != kModeHash;
   const SpanClock span_clk = span_begin(span);
   // Per quad two 128-byte message buffers.  Iteration i of the wave compresses from buffer
@@ -1427,17 +1428,17 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // A block in a run of quiet blocks (content hash only): every active quad is at least 4
   // blocks from its end, so nothing in it depends on a lane's position in its chain.  Runs
   // of these execute in their own loop, straight-line code between the round blocks.
-  // the fast loop's byte counter t (lane 0 only: ((blk + 1) << 7) & t_mask), advanced by one
-  // 64-bit add per block instead of rebuilt from blk (shift, add, two selects)
-  // Fair share (fair != nullptr, hash bins): the two waves of a SIMD hold equal work, but the
-  // SIMD's arbiter lets one run ahead (oldest first), which then ends early and leaves the
-  // other alone at the lone-wave rate.  At least every kFairEvery blocks each wave adds the
+  // Fair share (fair != nullptr): with hash bins the two waves of a SIMD hold equal work, but
+  // the SIMD's arbiter lets one run ahead (oldest first), which then ends early and leaves the
+  // other alone at the lone-wave rate.  At least every fair_every blocks each wave adds the
   // blocks it ran to a launch-wide counter and raises its issue priority while it is behind
   // the launch's average, so the waves of a SIMD advance together.
-  constexpr uint32_t kFairEvery = 256;
+  const uint32_t kFairEvery = fair_every ? fair_every : 256;
   uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; fair share, the trace)
   uint32_t reported = 0;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kHashBlock / 64);
+  // the fast loop's byte counter t (lane 0 only: ((blk + 1) << 7) & t_mask), advanced by one
+  // 64-bit add per block instead of rebuilt from blk (shift, add, two selects)
   uint64_t tm = 0;
   const uint64_t tinc = 128 & t_mask;
   auto fast_step = [&](auto par, uint64_t* pre) {
@@ -2083,6 +2084,16 @@ static uint32_t hash_prio_blocks() {
   return v;
 }
 
+// PFSCDC_HASH_FAIR_EVERY: blocks between a fair-share wave's priority updates (default 256)
+static uint32_t hash_fair_every() {
+  static const uint32_t v = [] {
+    const char* e = getenv("PFSCDC_HASH_FAIR_EVERY");
+    const int x = e ? atoi(e) : 0;
+    return (uint32_t)(x >= 8 && x <= 65536 ? x : 256);
+  }();
+  return v;
+}
+
 // Waves per SIMD for a hash launch.  One quad runs a chain's 128-B blocks strictly in order,
 // so no launch ends before its longest chain; a second wave on a SIMD only slows that chain
 // down (the two share the issue slots).  One wave per SIMD when the launch is bound by its
@@ -2134,7 +2145,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, dyn, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
       prio ? prio : hash_prio_blocks(), span, ordered ? next : nullptr,
-      ordered && next ? fair : nullptr);
+      ordered ? fair : nullptr, hash_fair_every());
   return hipGetLastError();
 }
 
@@ -2153,7 +2164,7 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
-      prio ? prio : hash_prio_blocks(), nullptr, next, nullptr);
+      prio ? prio : hash_prio_blocks(), nullptr, next, nullptr, 0u);
   return hipGetLastError();
 }
 
@@ -2186,7 +2197,7 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   blake2b_kernel<kModeGet><<<hash_grid(nsegs, num_cus, waves), kHashBlock, 0, st>>>(
       ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
-      nullptr, nullptr, nullptr);
+      nullptr, nullptr, nullptr, 0u);
   return hipGetLastError();
 }
 

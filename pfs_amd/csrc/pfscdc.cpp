@@ -160,11 +160,19 @@ bool hash_bins_enabled() {
   return on;
 }
 
-// PFSCDC_HASH_FAIR=0: hash bins without the fair-share issue priority (A/B)
+// PFSCDC_HASH_FAIR=0: hash bins without the fair-share issue priority; =2: fair share on LPT
+// launches without bins too (A/B)
 bool hash_fair_enabled() {
   static const bool on = [] {
     const char* e = getenv("PFSCDC_HASH_FAIR");
     return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+bool hash_fair_forced() {
+  static const bool on = [] {
+    const char* e = getenv("PFSCDC_HASH_FAIR");
+    return e && atoi(e) == 2;
   }();
   return on;
 }
@@ -538,7 +546,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
                              c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive(), next,
-                             hash_fair_enabled() ? c->d_counts.p + 5 : nullptr));
+                             hash_fair_enabled() && waves > 1 && (next || hash_fair_forced())
+                                 ? c->d_counts.p + 5 : nullptr));
   if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);

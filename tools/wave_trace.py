@@ -37,3 +37,10 @@ for k in range(len(raw) // rec):
           f"(x16 quads = {steps.sum() * 16:.4g} quad-block slots)")
     print(f"  SIMD-time idle after the SIMD's last wave: {np.sum(T - se_) / (len(se_) * T) * 100:.2f}%"
           f"; CU-time idle after the CU's last wave: {np.sum(T - ce) / (len(ce) * T) * 100:.2f}%")
+    # per XCD: when its SIMDs end (a slow XCD bounds a launch whose waves hold equal work)
+    ukey, inv = np.unique(simd_key, return_inverse=True)
+    m = np.zeros(len(ukey))
+    np.maximum.at(m, inv, end)
+    sx = (ukey // (8 * 2 * 16 * 4)).astype(int)
+    print("  per XCD: mean / max SIMD end (ms): " + "  ".join(
+        f"{x}: {m[sx == x].mean():.2f}/{m[sx == x].max():.2f}" for x in np.unique(sx)))
