@@ -300,9 +300,15 @@ def main():
     args = parse()
     # HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
     # share a queue and run one after the other: c3's four streams in flight (one context
-    # each) and the commit's two chunk sets need a queue per stream.  Set
-    # before the first HIP call; an explicit setting wins.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # each) and the commit's two chunk sets need a queue per stream.  Raised
+    # to 8 (the box exports 4) before the first HIP call; a larger setting is kept.
+    try:
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        q = 0
+    if q < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
     import numpy as np
     import torch
     import torch.distributed as dist
