@@ -178,7 +178,10 @@ int pfscdc_create_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
  * serial chains share the GPU instead of running one pass after the other; then
  * chunk.Create's dek and Ref.Id as pfscdc_create_refs.  refs as pfscdc_create_refs, or NULL:
  * then only the hashes (every BLAKE2b Writer.processChunk computes, writer.go:240,301-312)
- * and no chunk.Create.
+ * and no chunk.Create.  With refs and more chunks than the quads of one wave per SIMD, the
+ * long chunks (and their Ref.Ids) run on the ctx stream beside the rest on a second one, so
+ * their Ref.Id chains start as soon as their own content hashes are done (same results;
+ * PFSCDC_COMMIT_TWO_SETS=0/1 forces either form).
  * Synchronous; the scan's segment list is consumed (pfscdc_segments is empty afterwards). */
 int pfscdc_commit_refs(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int bytes_on_device,
                        const uint64_t* chunk_offsets, uint32_t nchunks, uint8_t* content_hashes,

@@ -856,6 +856,10 @@ static uint64_t commit_long_pct() {
   return (uint64_t)(x > 0 && x < 100 ? x : 30);
 }
 
+static bool commit_long_chains() {
+  const char* e = getenv("PFSCDC_COMMIT_LONG_CHAINS");
+  return e && atoi(e) != 0;
+}
 static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
   const char* e = getenv("PFSCDC_COMMIT_SHORT_WAVES");
   const int x = e ? atoi(e) : 0;
@@ -914,7 +918,18 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     sel[set_of[i]].push_back(i);
     if (!hash_known[i]) rec_chunk[set_of[i]].push_back(i);
   }
-  for (uint64_t s = 0; s < m; s++) rec_seg[set_of[seg_chunk[s]]].push_back(s);
+  // chains only (PFSCDC_COMMIT_LONG_CHAINS=1, A/B): the long set hashes only its chunks'
+  // content chains (a one-segment chunk's is its segment); the segments inside its
+  // multi-DataRef chunks go to the short set, and the long set's in-place ChaCha20 waits for
+  // the short set's hashes (they read those bytes).  Slower: its unions end sooner (240 vs 296
+  // ms on c4 G = 2) but the long set's chunk.Create then waits for the short set's, which holds
+  // every segment at one wave per SIMD (331 vs 362 GiB/s, profiles/r3/two_sets/chains_*)
+  const bool chains_only = commit_long_chains();
+  for (uint64_t s = 0; s < m; s++) {
+    const uint32_t i = seg_chunk[s];
+    const bool own = set_of[i] == 0 && (!chains_only || hash_known[i]);
+    rec_seg[own ? 0 : 1].push_back(s);
+  }
   HIP_OK(c, hipEventRecord(c->pev[0], c->stream));  // the scan and the bytes are ready
   HIP_OK(c, hipStreamWaitEvent(X[1]->stream, c->pev[0], 0));
   for (int x = 0; x < 2; x++) {
@@ -958,7 +973,8 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     if (R)
       HIP_OK(c, launch_blake2b(data, u->d_offs.p, u->d_segs.p, u->d_counts.p + 1, R, u->d_order.p,
                                u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
-                               x ? std::min(w, commit_short_waves()) : w, x ? kNoPrio : 1u));
+                               x ? std::min(w, commit_short_waves()) : chains_only ? 1 : w,
+                               x ? kNoPrio : 1u));
     if (R)
       HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
                                hipMemcpyDeviceToHost, st));
@@ -987,6 +1003,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
       u->cr_hash_prio = x ? kNoPrio : 1u;
       u->cr_chacha_prio = x == 0;
       u->cr_one_stream = true;  // each set has one stream (two in all)
+      if (x == 0 && chains_only) HIP_OK(c, hipStreamWaitEvent(c->stream, c->pev[2], 0));
       const int rc = create_refs_device(u, data, nbytes, co, nchunks, content_hashes, all.data(),
                                         refs, ct, sel[x].data(), (uint32_t)sel[x].size(), false);
       u->cr_wave_cap = 0;

@@ -166,8 +166,9 @@ def test_ciphertext_in_place_needs_device_bytes():
     c.close()
 
 
+@pytest.mark.parametrize("chains_only", ["0", "1"])
 @pytest.mark.parametrize("in_place", [False, True])
-def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, monkeypatch):
+def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkeypatch):
     """The two-set commit (the long chunks' hashes and chunk.Create on the ctx stream at issue
     priority, the rest on a helper context beside them, PFSCDC_COMMIT_TWO_SETS) gives the same
     DataRef hashes, content hashes, Refs and ciphertext as the one-pass form, at several
@@ -184,6 +185,8 @@ def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, monkeypatch):
     nf = len(lens)
     streams = [0, nf // 4, nf // 2, nf]
     cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+
+    monkeypatch.setenv("PFSCDC_COMMIT_LONG_CHAINS", chains_only)
 
     def run(two_sets, pct):
         monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "1" if two_sets else "0")
