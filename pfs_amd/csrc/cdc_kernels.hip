@@ -1197,6 +1197,32 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
   "v_xor_b32 v111, v103, v105\n"                                       \
   "v_alignbit_b32 v102, v110, v111, 31\n"                              \
   "v_alignbit_b32 v103, v111, v110, 31\n"
+// The first G of a block reading the block's initial state where it lives: a0 = h[j] and
+// b0 = h[4+j] (the chaining value, kept for the feed-forward), c0 = IV, and d0 ^ dt (IV with
+// the byte counter t in lane 0) as a 3-way XOR with a; the results land in the fixed
+// registers, so the block's set-up costs no moves (3 v_mov_b64 and 2 v_xor_b32 per block
+// before).  Outputs are early-clobber: no input may share v100-v107.
+#define PFS_G_ASM_FIRST(X, Y)                                          \
+  "v_lshl_add_u64 v[100:101], %[a0], 0, " X "\n"                      \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, %[b0]\n"                 \
+  "v_bitop3_b32 v108, %[d0h], %[dth], v101 bitop3:0x96\n"             \
+  "v_bitop3_b32 v109, %[d0l], %[dtl], v100 bitop3:0x96\n"             \
+  "v_lshl_add_u64 v[104:105], %[c0], 0, v[108:109]\n"                 \
+  "v_xor_b32 v110, %[b0l], v104\n"                                    \
+  "v_xor_b32 v111, %[b0h], v105\n"                                    \
+  "v_alignbit_b32 v102, v111, v110, 24\n"                             \
+  "v_alignbit_b32 v103, v110, v111, 24\n"                             \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, " Y "\n"                 \
+  "v_lshl_add_u64 v[100:101], v[100:101], 0, v[102:103]\n"            \
+  "v_xor_b32 v110, v108, v100\n"                                      \
+  "v_xor_b32 v111, v109, v101\n"                                      \
+  "v_alignbit_b32 v106, v111, v110, 16\n"                             \
+  "v_alignbit_b32 v107, v110, v111, 16\n"                             \
+  "v_lshl_add_u64 v[104:105], v[104:105], 0, v[106:107]\n"            \
+  "v_xor_b32 v110, v102, v104\n"                                      \
+  "v_xor_b32 v111, v103, v105\n"                                      \
+  "v_alignbit_b32 v102, v110, v111, 31\n"                             \
+  "v_alignbit_b32 v103, v111, v110, 31\n"
 #define PFS_QP_ID "[0,1,2,3]"
 #define PFS_QP_R1 "[1,2,3,0]"  // 0x39: lane j reads lane j+1
 #define PFS_QP_R2 "[2,3,0,1]"  // 0x4E
@@ -1210,6 +1236,17 @@ __global__ void dek_kernel(const pfscdc_segment* __restrict__ segs,
     [x1] "v"(x1_), [x2l] "v"((uint32_t)(x2_)), [x2h] "v"((uint32_t)((x2_) >> 32)),       \
     [x3] "v"(x3_)                                                                        \
   : "vcc", "v108", "v109", "v110", "v111"
+#define PFS_ROUND_FIRST(a0_, b0_, c0_, d0_, dt_, x0_, x1_, x2_, x3_)                          \
+  asm volatile(PFS_G_ASM_FIRST("%[x0]", "%[x1]") PFS_DIAG_G                                    \
+               : "=&{v[100:101]}"(a), "=&{v[102:103]}"(b), "=&{v[104:105]}"(c),                  \
+                 "=&{v[106:107]}"(d)                                                           \
+               : [a0] "v"(a0_), [b0] "v"(b0_), [b0l] "v"((uint32_t)(b0_)),                     \
+                 [b0h] "v"((uint32_t)((b0_) >> 32)), [c0] "v"(c0_),                            \
+                 [d0l] "v"((uint32_t)(d0_)), [d0h] "v"((uint32_t)((d0_) >> 32)),               \
+                 [dtl] "v"((uint32_t)(dt_)), [dth] "v"((uint32_t)((dt_) >> 32)),               \
+                 [x0] "v"(x0_), [x1] "v"(x1_), [x2l] "v"((uint32_t)(x2_)),                      \
+                 [x2h] "v"((uint32_t)((x2_) >> 32)), [x3] "v"(x3_)                              \
+               : "vcc", "v108", "v109", "v110", "v111")
 #define PFS_ROUND(FIRST, x0_, x1_, x2_, x3_)                                                  \
   do {                                                                                        \
     if (FIRST)                                                                                \
@@ -1364,7 +1401,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // pre (optional): round 0's message words, already read (the quiet-run loop reads the next
   // block's at round 11 into pre, from the buffer round 5 staged it in).
   auto rounds = [&](auto par, uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
-                    auto&& put_next, uint64_t* pre = nullptr, bool back = true) {
+                    auto&& put_next, uint64_t* pre = nullptr, bool back = true,
+                    uint64_t dt = 0) {  // the first G takes d ^ dt
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1402,6 +1440,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         pre[3] = lds_abs_u64(ma[0][3] + nxt);
       }
 #ifdef PFS_HASH_CXX
+      if (r == 0) d ^= dt;
       PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
       a = quad_perm64<0x93>(a);            // a <- v[(j+3)%4]
       c = quad_perm64<0x39>(c);            // c <- v[8+(j+1)%4]
@@ -1411,7 +1450,12 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       c = quad_perm64<0x93>(c);
       d = quad_perm64<0x4E>(d);
 #else
-      PFS_ROUND(r == 0, x0, x1, x2, x3);   // leaves a, c, d in the diagonal layout
+      if (r == 0) {  // leaves a, c, d in the diagonal layout
+        const uint64_t a0 = a, b0 = b, c0 = c, d0 = d;
+        PFS_ROUND_FIRST(a0, b0, c0, d0, dt, x0, x1, x2, x3);
+      } else {
+        PFS_ROUND(false, x0, x1, x2, x3);
+      }
 #endif
       x0 = y0; x1 = y1; x2 = y2; x3 = y3;
       if (r == 5) put_next();
@@ -1443,13 +1487,13 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   const uint64_t tinc = 128 & t_mask;
   auto fast_step = [&](auto par, uint64_t* pre) {
     constexpr uint32_t cur = decltype(par)::value * kMsgBuf, nxt = kMsgBuf - cur;
-    uint64_t a = ha, b = hb, c = iv_c, d = iv_d ^ tm;
+    uint64_t a = ha, b = hb, c = iv_c, d = iv_d;  // d ^ tm in the first G
     rounds(par, a, b, c, d, [&] {
       if (active) {
         lds_put(nxt);
         msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
       }
-    }, pre, false);
+    }, pre, false, tm);
     fold_diag(ha, hb, a, b, c, d);
     tm += tinc;
     blk++;  // inactive quads too: a refill resets blk
