@@ -2145,12 +2145,9 @@ static uint32_t hash_fair_every() {
 // c3, c4, a single configs[1] batch, most chunk.Create passes), two otherwise (c2's 128 GiB
 // steps: 72 vs 80 ms; c4: 100 vs 104-110 ms).  PFSCDC_HASH_WAVES=n forces n (A/B).
 int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus) {
-  static const int forced = [] {
-    const char* e = getenv("PFSCDC_HASH_WAVES");
-    const int w = e ? atoi(e) : 0;
-    return w >= 1 && w <= 8 ? w : 0;
-  }();
-  if (forced) return forced;
+  const char* e = getenv("PFSCDC_HASH_WAVES");  // read per launch (tests switch it)
+  const int forced = e ? atoi(e) : 0;
+  if (forced >= 1 && forced <= 8) return forced;
   const uint64_t quads1 = (uint64_t)num_cus * 4 * (64 / 4);
   const uint64_t longest = (longest_bytes + 127) / 128, total = total_bytes / 128;
   return longest * quads1 >= total ? 1 : kHashWavesPerSimd;

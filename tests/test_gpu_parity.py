@@ -267,14 +267,17 @@ def test_kernel_spans_and_clocks_are_recorded():
     c.close()
 
 
+@pytest.mark.parametrize("waves", ["1", "2"])
 @pytest.mark.parametrize("bin_bytes", ["0", "60000", "1000000000000"])
 @pytest.mark.parametrize("ref_ids", [False, True])
-def test_hash_bins_equal_oracle(bin_bytes, ref_ids, monkeypatch):
+def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
     """Hash bins (a quad hashes every segment of a file of at most bin_bytes back to back,
     lpt_order_block): digests, and with PFSCDC_OPT_REF_IDS the per-segment Ref.Ids, equal to
     the oracle whether no file, some files or every file forms a bin (empty files and files
-    cut into many segments included)."""
+    cut into many segments included); at two waves per SIMD the hash launch also runs the
+    fair-share issue priority (its launch-wide counter and the capped quiet countdown)."""
     monkeypatch.setenv("PFSCDC_HASH_BIN_BYTES", bin_bytes)
+    monkeypatch.setenv("PFSCDC_HASH_WAVES", waves)
     rng = np.random.default_rng(5)
     lens = np.concatenate([rng.integers(0, 70_000, 200), [0, 0, 1, 30_000, 250_000, 0]])
     rng.shuffle(lens)
