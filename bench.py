@@ -99,7 +99,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps in flight (one GPU context + input buffer each; --path commit: "
                          "one context + host thread each over the step's one input buffer); "
-                         "0 = auto: 4 for --path put on c3 (fewer if HBM cannot hold them), else 1")
+                         "0 = auto: 4 for --path put on c3, 2 on c4/c5 (fewer if HBM cannot hold "
+                         "them), else 1")
     ap.add_argument("--hash-order", default="free", choices=["serial", "free"],
                     help="steps in flight: serial = a step's hash kernel starts after the "
                          "previous step's (scans overlap hash tails; each hash launch has the "
@@ -360,10 +361,13 @@ def main():
     # duration (HIP events, in-kernel span and a kernel trace alike) is its own.  c3 (one
     # stream, bound by its longest 20 MB chains: ~175 ms per stream whatever else runs) runs
     # four steps in flight on four contexts (one hardware queue each, GPU_MAX_HW_QUEUES);
+    # c4/c5 two (the next commit's scan and hashes fill what the chain-bound hash leaves:
+    # 824 -> 936 / 820 -> 883 GiB/s, profiles/r3/c4_inflight/);
     # c2's two-in-flight throughput is measured after the timed region (``two_in_flight``).
     # c4/c5 hold >= 16K chains per step through --group instead.
     S = args.inflight if args.inflight > 0 else (
-        4 if args.path == "put" and args.config == "c3" else 1)
+        4 if args.path == "put" and args.config == "c3" else
+        2 if args.path == "put" and args.config in ("c4", "c5") else 1)
     batches = []
     for k in range(S):
         try:
