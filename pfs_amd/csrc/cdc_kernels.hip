@@ -1693,6 +1693,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     g_wave_trace[4 * w] = __builtin_amdgcn_s_memrealtime();
     g_wave_trace[4 * w + 1] = (uint64_t)hw | ((uint64_t)xcc << 32);
     g_wave_trace[4 * w + 2] = wave_steps;
+    g_wave_trace[4 * w + 3] = __builtin_amdgcn_s_memtime() - span_clk.t0;  // shader cycles
   }
   span_end(span, span_clk);
 }

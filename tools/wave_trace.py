@@ -1,6 +1,7 @@
 """Read a PFSCDC_WAVE_TRACE file (development tool): per hash launch, how the waves, SIMDs and
 CUs of the launch drain.  Each record: span[4] (scan begin/end, hash begin/end; s_memrealtime
-ticks, 100 MHz) then 32768 x (end tick, HW_ID | XCC_ID << 32, blocks run, 0) per wave slot."""
+ticks, 100 MHz) then 32768 x (end tick, HW_ID | XCC_ID << 32, blocks run, shader cycles) per
+wave slot."""
 import sys
 
 import numpy as np
@@ -44,3 +45,9 @@ for k in range(len(raw) // rec):
     sx = (ukey // (8 * 2 * 16 * 4)).astype(int)
     print("  per XCD: mean / max SIMD end (ms): " + "  ".join(
         f"{x}: {m[sx == x].mean():.2f}/{m[sx == x].max():.2f}" for x in np.unique(sx)))
+    cyc = w[:, 3].astype(np.float64)
+    if cyc.any():  # each wave's lifetime in shader cycles over its wall time: its clock
+        mhz = cyc / np.maximum(end, 1e-3) / 1e3
+        wx = ((simd_key // (8 * 2 * 16 * 4)).astype(int))
+        print("  per XCD: mean wave clock (MHz): " + "  ".join(
+            f"{x}: {mhz[wx == x].mean():.0f}" for x in np.unique(wx)))
