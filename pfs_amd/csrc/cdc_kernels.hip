@@ -2201,9 +2201,11 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
                           uint8_t* ctext_out, hipStream_t st, int waves, uint32_t prio,
-                          const uint32_t* next) {
+                          const uint32_t* next, const uint64_t* nsegs) {
   if (max_segments == 0) return hipSuccess;
-  dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(segs, seg_count, refs, counter);
+  // a dek for every segment (nsegs; with hash bins seg_count is the queue's length)
+  dek_kernel<<<(unsigned)((max_segments + 255) / 256), 256, 0, st>>>(
+      segs, nsegs ? nsegs : seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
       prio ? prio : hash_prio_blocks(), nullptr, next, nullptr, 0u);

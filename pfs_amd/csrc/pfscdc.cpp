@@ -554,7 +554,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (c->have_refs && nfiles)
     HIP_OK(c, launch_ref_ids(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p + 1, c->num_cus, nbytes, c->d_refs.p,
-                             nullptr, st, waves, 0u, next));
+                             nullptr, st, waves, 0u, next, c->d_seg_begin.p + nfiles));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, c->h_seg_begin.ensure(nfiles + 1));
   if (nfiles)
@@ -910,6 +910,18 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
   for (auto& e : c->pev)
     if (!e) HIP_OK(c, hipEventCreate(&e));
   pfscdc_ctx* const X[2] = {c, c->helper};
+  // any early return below (a HIP error) first drains both streams, so no launch of this call
+  // still reads the caller's bytes or the ctxs' buffers after it returns
+  struct DrainOnReturn {
+    hipStream_t a, b;
+    bool armed = true;
+    ~DrainOnReturn() {
+      if (armed) {
+        (void)hipStreamSynchronize(a);
+        (void)hipStreamSynchronize(b);
+      }
+    }
+  } drain{c->stream, X[1]->stream};
   // per set: its chunks; its union records (content hashes of its multi-DataRef chunks, then
   // every segment inside its chunks)
   std::vector<uint32_t> sel[2], rec_chunk[2];
@@ -1011,10 +1023,8 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
       u->cr_chacha_prio = false;
       u->cr_one_stream = false;
       if (rc) {
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(X[1]->stream);
         if (x) c->err = X[1]->err;
-        return rc;
+        return rc;  // drain waits for both streams
       }
       done[x] = progressed = true;
     }
@@ -1032,6 +1042,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     if (hipEventElapsedTime(&ms, c->pev[0], c->pev[1 + x]) == hipSuccess) a = std::max(a, ms);
   for (int x = 0; x < 2; x++)
     if (hipEventElapsedTime(&ms, c->pev[0], X[x]->ev[6]) == hipSuccess) b = std::max(b, ms);
+  drain.armed = false;  // create_refs_finish waited for both streams
   c->create_hash_ms = a;  // both sets' hashes (they overlap the long set's Ref.Id pass)
   c->create_ms = b;
   c->scan_valid = false;

@@ -138,7 +138,8 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, const uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, pfscdc_ref* refs,
                           uint8_t* ctext_out, hipStream_t st, int waves = 0, uint32_t prio = 0,
-                          const uint32_t* next = nullptr);
+                          const uint32_t* next = nullptr,  // hash bins: seg_count = queue length
+                          const uint64_t* nsegs = nullptr);  // then: the segment count (deks)
 // dek per record (refs[].dek from segs[].hash); zeroes *counter
 hipError_t launch_deks(pfscdc_segment* segs, const uint64_t* seg_count, uint64_t max_segments,
                        pfscdc_ref* refs, uint32_t* counter, hipStream_t st);

@@ -286,11 +286,11 @@ def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
     c = Chunker(cp(SMALL), device=0, ref_ids=ref_ids)
     res = c.scan(data, offs)
     assert_same(res, data, offs, SMALL)
-    if ref_ids:
-        refs = res.refs
-        for i in np.linspace(0, len(res.segments) - 1, 10).astype(int):
+    if ref_ids:  # every segment (a sample once hid deks missing past the queue's length:
+        refs = res.refs  # a fresh ctx can get the device memory of a previous correct run)
+        for i in range(len(res.segments)):
             g = res.segments[i]
             a = int(offs[g["file"]] + g["offset"])
             rid, dek = Ch.create_ref_id(data[a:a + int(g["size"])].tobytes())
-            assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek
+            assert bytes(refs[i]["dek"]) == dek and bytes(refs[i]["id"]) == rid, i
     c.close()
