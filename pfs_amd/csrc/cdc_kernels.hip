@@ -39,7 +39,7 @@
 // LDS address permute or the DMA wait: they produce wrong cuts and digests, so a build that
 // defines one must also say so explicitly; the product Makefile never does.
 #if defined(PFS_EXP_NO_TABLE) || defined(PFS_EXP_NO_ROT) || defined(PFS_EXP_NO_PERM) || \
-    defined(PFS_EXP_NO_DMA_WAIT)
+    defined(PFS_EXP_NO_DMA_WAIT) || defined(PFS_EXP_MSG_SAME)
 #ifndef PFS_TIMING_ONLY_BUILD
 #error "PFS_EXP_NO_* knobs give wrong results: define PFS_TIMING_ONLY_BUILD for a timing-only build"
 #endif
@@ -1491,7 +1491,11 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     rounds(par, a, b, c, d, [&] {
       if (active) {
         lds_put(nxt);
+#ifdef PFS_EXP_MSG_SAME  // timing only: every fast block loads the segment's first block (L2)
+        msg_load_full(m0, m1, src + 32 * j);
+#else
         msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
+#endif
       }
     }, pre, false, tm);
     fold_diag(ha, hb, a, b, c, d);
