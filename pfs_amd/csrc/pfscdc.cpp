@@ -860,6 +860,16 @@ static bool commit_long_chains() {
   const char* e = getenv("PFSCDC_COMMIT_LONG_CHAINS");
   return e && atoi(e) != 0;
 }
+static int commit_long_waves() {  // PFSCDC_COMMIT_LONG_WAVES: the long set's (0: its own)
+  const char* e = getenv("PFSCDC_COMMIT_LONG_WAVES");
+  const int x = e ? atoi(e) : 0;
+  return x >= 1 && x <= 2 ? x : 0;
+}
+static int commit_long_create_waves() {  // PFSCDC_COMMIT_LONG_CREATE_WAVES (0: its own)
+  const char* e = getenv("PFSCDC_COMMIT_LONG_CREATE_WAVES");
+  const int x = e ? atoi(e) : 0;
+  return x >= 1 && x <= 2 ? x : 0;
+}
 static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
   const char* e = getenv("PFSCDC_COMMIT_SHORT_WAVES");
   const int x = e ? atoi(e) : 0;
@@ -985,7 +995,8 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     if (R)
       HIP_OK(c, launch_blake2b(data, u->d_offs.p, u->d_segs.p, u->d_counts.p + 1, R, u->d_order.p,
                                u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
-                               x ? std::min(w, commit_short_waves()) : chains_only ? 1 : w,
+                               x ? std::min(w, commit_short_waves())
+                                 : chains_only ? 1 : commit_long_waves() ? commit_long_waves() : w,
                                x ? kNoPrio : 1u));
     if (R)
       HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
@@ -1011,7 +1022,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
       for (uint32_t i : sel[x])
         if (hash_known[i])
           std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * known_seg[i], 32);
-      u->cr_wave_cap = x ? commit_short_waves() : 0;
+      u->cr_wave_cap = x ? commit_short_waves() : commit_long_create_waves();
       u->cr_hash_prio = x ? kNoPrio : 1u;
       u->cr_chacha_prio = x == 0;
       u->cr_one_stream = true;  // each set has one stream (two in all)
