@@ -425,13 +425,19 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
         dma_off[i] = r * strip + 16u * ((lane & 7u) ^ stage_swz(r));
       }
       const bool fast = wave_base + 64 * (uint64_t)strip <= n_main;
+      // the unit's bytes as a raw buffer (SGPR descriptor: base = the unit's first byte; every
+      // offset is below 256 KiB): the fast path's DMA is buffer_load ... lds with the lane's
+      // 32-bit offset and the step in soffset, no 64-bit address add per instruction (8 VALU
+      // per 128-B step with global_load_lds)
+      const __amdgpu_buffer_rsrc_t unit_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(data + wave_base), (short)0, 0x7fffffff, 0x00020000);
       auto dma_step = [&](uint32_t step) {
-        if (fast) {  // wave-uniform: a scalar base plus the lane's 32-bit offset, LDS dst in M0
-          const uint8_t* base = data + (wave_base + step * 128u);
+        if (fast) {  // wave-uniform: descriptor + soffset in SGPRs, LDS dst in M0
 #pragma unroll
           for (int i = 0; i < 8; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(base + dma_off[i]),
-                (__attribute__((address_space(3))) void*)(wbuf + i * 1024), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                unit_rsrc, (__attribute__((address_space(3))) void*)(wbuf + i * 1024), 16,
+                dma_off[i], step * 128u, 0, 0);
           return;
         }
 #pragma unroll
