@@ -1,4 +1,5 @@
 #!/bin/bash
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3c4_parity.log 2>&1 || { tail -30 gpurun_out/r3c4_parity.log; exit 1; }; tail -1 gpurun_out/r3c4_parity.log
 # round 3: c4 / c5 with one and two commits in flight (two contexts), 8 hardware queues
 mkdir -p gpurun_out/r3c4
 o=gpurun_out/r3c4
