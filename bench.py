@@ -89,7 +89,7 @@ def parse():
                     help="--path uw: group writers in flight (PFSCDC_UW_WORKERS; default 1)")
     ap.add_argument("--uw-group", type=int, default=0,
                     help="--path uw: bytes of serialized filesets per group write "
-                         "(PFSCDC_UW_INFLIGHT; default 8 GiB)")
+                         "(PFSCDC_UW_INFLIGHT; default 32 GiB)")
     ap.add_argument("--rechunk-writers", type=int, default=10,
                     help="rechunk: writers the file was written by (TestStableHash shape)")
     ap.add_argument("--mem-threshold", type=int, default=10 ** 9,

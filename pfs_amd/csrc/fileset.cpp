@@ -623,13 +623,15 @@ void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) { CopyPool::get
 
 // Page-locked arenas outlive their writer: a commit creates a fresh UnorderedWriter, and
 // page-locking 1 GB for every fileset of every commit (hipHostMalloc) costs more than the Put
-// copies themselves.  Process-wide pool, at most PFSCDC_UW_ARENA_POOL arenas (default 16).
+// copies themselves.  Process-wide pool, at most PFSCDC_UW_ARENA_POOL arenas (default 40:
+// one 32 GiB group's worth, so a group never page-locks fresh arenas; with 16 a 32 GiB group
+// re-allocated 18 of them every commit, 11.7 vs 27.8 GiB/s, profiles/r3/uw_groups/).
 struct ArenaPool {
   std::mutex mu;
   std::vector<std::unique_ptr<Arena>> free;
   size_t cap = [] {
     const char* e = getenv("PFSCDC_UW_ARENA_POOL");
-    return e ? (size_t)std::max(0, atoi(e)) : (size_t)16;
+    return e ? (size_t)std::max(0, atoi(e)) : (size_t)40;
   }();
   std::unique_ptr<Arena> take(uint64_t bytes, int device) {
     std::lock_guard<std::mutex> lk(mu);
@@ -696,7 +698,10 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   // Serialized buffers waiting for the GPU: up to inflight_bytes of them are written
   // together (one scan, one hash launch and one chunk.Create for all their data streams) by
   // one of the group writers, round robin, while Puts continue.  The output equals
-  // serializing one at a time; each fileset's chunk stream is independent.
+  // serializing one at a time; each fileset's chunk stream is independent.  A group's GPU
+  // time is bound by its longest chunks' two serial chains (~340 ms on c4) whatever its size,
+  // so groups are large: 32 GiB (PFSCDC_UW_INFLIGHT; c4, 32 GiB Put: 8 GiB groups 18.8, 16
+  // GiB 25.1, 32 GiB 27.8 GiB/s, profiles/r3/uw_groups/).
   std::vector<Buffer> pending;
   std::vector<std::unique_ptr<Arena>> pool;  // arenas of written filesets, for reuse
   std::mutex pool_mu;
@@ -717,7 +722,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     return !(e && atoi(e) == 0);
   }();
   hipStream_t up_stream = nullptr;  // the Puts' uploads into the arena mirrors
-  uint64_t pending_bytes = 0, inflight_bytes = 8ull << 30;
+  uint64_t pending_bytes = 0, inflight_bytes = 32ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
                         std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
   uint32_t next_fileset = 0;
