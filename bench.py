@@ -182,12 +182,14 @@ def workload(args, world, rank):
     if args.config == "c2":
         G = args.group if args.group > 0 else 32
         n = args.files * G
-        seed = (0xC2 if args.seed < 0 else args.seed) + 1000 * rank
+        seed = 0xC2 if args.seed < 0 else args.seed
         info = {"workload": "configs[1]: batches of %d x %d B independent buffers; %d batches "
                             "per step (one launch group) per GPU" % (args.files, args.file_bytes, G),
                 "files_per_step": n, "file_bytes": args.file_bytes, "batches_per_step": G}
-        return Work([args.file_bytes] * n, np.arange(n), np.zeros(n), seed, SYNTH_RANDOM, info,
-                    "weak", gbase=rank * n, group=G, per_copy=args.files)
+        # rank r holds global files [r n, (r + 1) n) of one synthetic file sequence, so N ranks
+        # at G batches each cover the same files as one GPU at N G batches: equal index digests
+        return Work([args.file_bytes] * n, np.arange(n) + rank * n, np.zeros(n), seed,
+                    SYNTH_RANDOM, info, "weak", gbase=rank * n, group=G, per_copy=args.files)
     if args.config == "c3":
         seed = 0xC3 if args.seed < 0 else args.seed
         a, b = pd.split_stream(C3_BYTES, world)[rank]
@@ -297,18 +299,59 @@ def med(xs):
     return round(statistics.median(xs), 4) if xs else None
 
 
-def main():
-    args = parse()
-    # HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
-    # share a queue and run one after the other: c3's four streams in flight (one context
-    # each) and the commit's two chunk sets need a queue per stream.  Raised
-    # to 8 (the box exports 4) before the first HIP call; a larger setting is kept.
+def needs_launch(gpus: int, env) -> bool:
+    """--gpus N > 1 without a launcher's WORLD_SIZE: this process starts the N ranks itself."""
+    return gpus > 1 and "WORLD_SIZE" not in env
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(gpus: int, argv, port: int, python: str = sys.executable):
+    """torch.distributed.run over this script with the same arguments: one rank per GPU of
+    this node, rendezvous on 127.0.0.1."""
+    return [python, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+            str(gpus), "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Start the N ranks as a CHILD process (this process has imported nothing that touches
+    the GPU and never execs); rank 0's JSON line reaches our stdout through the inherited
+    descriptor.  Returns the launcher's exit code."""
+    import subprocess
+    cmd = launch_command(gpus, argv, free_port())
+    print("launching %d ranks: %s" % (gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def hw_queues_setting() -> int:
+    """HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
+    share a queue and run one after the other: c3's four streams in flight (one context
+    each) and the commit's two chunk sets need a queue per stream.  Raised
+    to 8 (the box exports 4) before the first HIP call; a larger setting is kept.  The
+    effective value goes into the line's config."""
     try:
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
     except ValueError:
         q = 0
     if q < 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        q = 8
+    return q
+
+
+def main():
+    args = parse()
+    if needs_launch(args.gpus, os.environ):
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    hwq = hw_queues_setting()
 
     import numpy as np
     import torch
@@ -336,7 +379,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     cdev = None if rehearse else dev  # collectives' tensors: device (RCCL) or host (gloo)
     ctx = {"np": np, "torch": torch, "dist": dist, "dev": dev, "cdev": cdev, "world": world,
-           "rank": rank, "local": local, "pd": pd}
+           "rank": rank, "local": local, "pd": pd, "hwq": hwq}
 
     params = ChunkParams()  # reference defaults: avgBits 23, seed 1, min 1 MB, max 20 MB
     ctx["params"] = params
@@ -401,13 +444,12 @@ def main():
         return bench_get(args, ctx, chunkers[0], batches[0], work)
 
     chunker, data = chunkers[0], batches[0]
-    # all_gather_into_tensor needs equal blocks: the capacity of the largest shard
-    cap = max(pd.max_segments(workload(args, world, r).sizes, params.min_chunk)
-              for r in range(world)) if world > 1 else 0
     gather = world > 1 or args.config != "c2"  # the commit's / stream's index on rank 0
     torch.cuda.synchronize()
     steps_t = []   # per timed step: the library's timings dict
     done_at = []   # completion times of the timed steps
+    gather_ms = []  # per timed step: the index gather to rank 0 (host wall clock)
+    gstats = {}
     pending = [False] * NC
     last = {}
 
@@ -417,7 +459,14 @@ def main():
         if gather:
             segs = res.segments.copy()
             segs["file"] = work.gid[segs["file"]].astype(np.uint32)
-            last["index"] = pd.gather_index(segs, 0, cap, device=cdev) if world > 1 else segs
+            if world > 1:
+                # counts first, then each rank's live records point to point to rank 0
+                g0 = time.perf_counter()
+                last["index"] = pd.gather_index_to_root(segs, device=cdev, stats=gstats)
+                if record:
+                    gather_ms.append((time.perf_counter() - g0) * 1e3)
+            else:
+                last["index"] = segs
         if record:
             steps_t.append(chunkers[k].timings())
             done_at.append(time.perf_counter())
@@ -530,9 +579,11 @@ def main():
     info.update({"steps_in_flight": S, "host_ahead": ahead,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},
-                 "parallelism": ("file-sharded x%d, RCCL all-gather of chunk-ref index" % world
-                                 if args.config == "c2" else
-                                 "fileset-sharded x%d, RCCL all-gather of chunk-ref index" % world)
+                 "gpu_max_hw_queues": ctx["hwq"],
+                 "parallelism": ("%s-sharded x%d, chunk-ref index gathered to rank 0 every "
+                                 "step (%s: counts all-gathered, live records sent point to "
+                                 "point)" % ("file" if args.config == "c2" else "fileset",
+                                             world, "gloo" if rehearse else "RCCL"))
                  if world > 1 else "single GPU"})
     out = {
         "metric": "GiB/s device-resident CDC rolling-hash + chunk content-hash",
@@ -584,16 +635,34 @@ def main():
         # the literal configuration beside the grouped one: ONE commit per step over the N GPUs
         # (copy 0 of this rank's share: strong scaling, bound by its longest chains)
         out["single_commit"] = single_commit(args, work, chunkers[0], batches[0], ctx)
-    if gather and rank == 0 and "index" in last:
+    if rank == 0 and not gather:  # c2 at N = 1: the step's own index
+        idx = res.segments.copy()
+        idx["file"] = work.gid[idx["file"]].astype(np.uint32)
+        last["index"] = idx
+    if rank == 0 and "index" in last:
         idx = last["index"]
         if args.config in ("c4", "c5"):  # the commit itself: copy 0 of every rank
             idx = idx[idx["file"] < work.layout.npieces]
         if args.config == "c5":
             out["dedup"] = hit_rate(idx)
-        # the gathered chunk-ref index of the commit / stream: equal at every N
+        # the gathered chunk-ref index of the commit / stream: equal at every N (c2: N ranks
+        # at G batches each = one GPU at N G batches)
         out["index_digest"] = __import__("hashlib").blake2b(idx.tobytes(),
                                                             digest_size=16).hexdigest()
         out["index_segments"] = int(len(idx))
+        if world > 1:
+            live = int(gstats.get("records", 0)) * idx.dtype.itemsize
+            out["index_gather"] = {
+                "how": "all-gather of the 8-byte counts, then each rank's live records sent "
+                       "point to point to rank 0 (no padding, no other receiver)",
+                "backend": "gloo" if rehearse else "nccl (RCCL)",
+                "records_per_step": int(gstats.get("records", 0)),
+                "live_record_bytes_per_step": live,
+                "bytes_received_by_rank0_per_step": int(gstats.get("bytes_received", 0)),
+                "count_bytes_per_rank": 8 * world,
+                "moved_over_live": round((gstats.get("bytes_received", 0) + 8 * world * world)
+                                         / max(live, 1), 4),
+                "ms_median": med(gather_ms)}
 
     # the timed steps are done: release the other steps' inputs and contexts (the e2e
     # contexts below allocate their own device copies)
@@ -1184,12 +1253,16 @@ def bench_commit(args, ctx):
         crec["dek"] = last["refs"]["dek"][:nch]
     else:
         crec["id"] = last["chash"][:nch]
-    chunks = pd.gather_records(crec, device=cdev) if world > 1 else crec
+    chunks = pd.gather_records_to_root(crec, device=cdev) if world > 1 else crec
+    if chunks is None:  # not rank 0: nothing gathered here, nothing printed
+        chunks = crec[:0]
     segs0 = last["res"].segments
     segs0 = segs0[segs0["file"] < per_copy]
     dr_hashes = np.ascontiguousarray(segs0["hash"]).view(np.dtype((np.void, 32))).reshape(-1)
     if world > 1:  # the commit's DataRef hashes in commit order: equal at every N
-        dr_hashes = pd.gather_records(dr_hashes, device=cdev)
+        dr_hashes = pd.gather_records_to_root(dr_hashes, device=cdev)
+        if dr_hashes is None:
+            dr_hashes = np.zeros(0, dtype=np.dtype((np.void, 32)))
     info = dict(work.info)
     info.update({"path": "commit (UnorderedWriter filesets -> chunk.Writer streams -> "
                          "chunk.Create)", "mem_threshold": args.mem_threshold,
@@ -1200,8 +1273,8 @@ def bench_commit(args, ctx):
                  "ciphertext_in_place": in_place,
                  "chunk_create": not args.no_create,
                  "commit_hash": args.commit_hash,
-                 "steps_in_flight": S,
-                 "parallelism": "fileset-sharded x%d, all-gather of the chunk records" % world
+                 "steps_in_flight": S, "gpu_max_hw_queues": ctx["hwq"],
+                 "parallelism": "fileset-sharded x%d, chunk records gathered to rank 0" % world
                  if world > 1 else "single GPU"})
     ms = avg["create"]
     ach = total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -1327,7 +1400,7 @@ def bench_uw(args, ctx):
             "path": "uw (host-fed UnorderedWriter -> fileset.Writer -> index.Writer)",
             "bytes_this_rank": nbytes, "mem_threshold": args.mem_threshold,
             "filesets": lay.nfilesets, "filesets_this_rank": len(prims),
-            "data_chunks_this_rank": nchunks,
+            "data_chunks_this_rank": nchunks, "gpu_max_hw_queues": ctx["hwq"],
             "parallelism": "fileset-sharded x%d, all-gather of the fileset roots" % world
             if world > 1 else "single GPU"}
     out = {

@@ -435,7 +435,7 @@ int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int appe
 int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag);
 int pfscdc_uw_close(pfscdc_uwriter* w); /* serializes the rest (Close, :171-179) */
 /* Serialized filesets are written in groups of up to PFSCDC_UW_INFLIGHT bytes (env, default
- * 8 GiB) on a background thread while Puts continue; the event callback may run on that
+ * 32 GiB) on a background thread while Puts continue; the event callback may run on that
  * thread (one group at a time, events in order).  Filesets are readable after Close. */
 uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w);
 /* Fileset i's Primitive (pointers valid until pfscdc_uw_destroy). */
@@ -453,6 +453,19 @@ const char* pfscdc_uw_last_error(const pfscdc_uwriter* w);
  * out[6] the data chunks' callbacks; out[7] the index writers; out[8] the group writes'
  * wall time. */
 int pfscdc_uw_timings(const pfscdc_uwriter* w, double out[9]);
+
+/* Memory the writers keep for the next writer (no reference counterpart: a GPU-side cache).
+ * Each fileset's page-locked host arena (memThreshold bytes) and its device mirror (as many
+ * bytes of HBM) go to a process-wide pool when the writer is destroyed, up to
+ * PFSCDC_UW_ARENA_POOL_BYTES (env, default 40e9 host bytes + as many device bytes); the
+ * contexts a writer made for itself (index levels, extra group writers), with their grow-only
+ * device staging, go to a cache of up to PFSCDC_CTX_CACHE (default 32) contexts.  Both count
+ * against the device memory other calls see (pfscdc_commit_refs takes its ciphertext copy only
+ * with 8 GiB to spare).  pfscdc_uw_trim_cache frees the pooled arenas and destroys the cached
+ * contexts of one device (-1: all devices); call it when no writer is being created or
+ * destroyed.  pfscdc_uw_cached_arena_bytes: host bytes of the pooled arenas now. */
+int pfscdc_uw_trim_cache(int device, uint64_t* arena_bytes_freed, uint32_t* ctxs_destroyed);
+uint64_t pfscdc_uw_cached_arena_bytes(void);
 
 /* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
 int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);

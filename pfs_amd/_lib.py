@@ -44,6 +44,7 @@ EXPORTED = [
     "pfscdc_create_refs", "pfscdc_last_create_ms", "pfscdc_form_chunks",
     "pfscdc_uw_create", "pfscdc_uw_put", "pfscdc_uw_delete", "pfscdc_uw_close",
     "pfscdc_uw_num_filesets", "pfscdc_uw_fileset", "pfscdc_uw_destroy", "pfscdc_uw_last_error", "pfscdc_uw_timings",
+    "pfscdc_uw_trim_cache", "pfscdc_uw_cached_arena_bytes",
     "pfscdc_path_clean",
     "pfscdc_hash_data_refs", "pfscdc_store_create", "pfscdc_store_destroy", "pfscdc_store_put",
     "pfscdc_store_get", "pfscdc_store_count", "pfscdc_writer_set_store", "pfscdc_writer_copy",
@@ -214,6 +215,8 @@ def load() -> C.CDLL:
             "pfscdc_uw_destroy": (i32, [vp]),
             "pfscdc_uw_last_error": (C.c_char_p, [vp]),
             "pfscdc_uw_timings": (i32, [vp, P(C.c_double)]),
+            "pfscdc_uw_trim_cache": (i32, [i32, P(u64), P(u32)]),
+            "pfscdc_uw_cached_arena_bytes": (u64, []),
             "pfscdc_path_clean": (i32, [C.c_char_p, i32, C.c_char_p, u64]),
             "pfscdc_hash_data_refs": (i32, [vp, vp, u32, vp]),
             "pfscdc_store_create": (i32, [P(vp)]),

@@ -231,6 +231,21 @@ struct CtxCache {
     }
     return c;
   }
+  // Destroy the cached contexts of one device (-1: all): their streams, events and grow-only
+  // device staging (a group write's whole input and ciphertext).
+  uint32_t trim(int device) {
+    std::vector<pfscdc_ctx*> out;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = free.size(); i-- > 0;)
+        if (device < 0 || pfscdc::ctx_device(free[i].second) == device) {
+          out.push_back(free[i].second);
+          free.erase(free.begin() + (ptrdiff_t)i);
+        }
+    }
+    for (pfscdc_ctx* c : out) pfscdc_ctx_destroy(c);
+    return (uint32_t)out.size();
+  }
   void give(pfscdc_ctx* c) {
     if (!c) return;
     std::unique_lock<std::mutex> lk(mu);
@@ -623,15 +638,21 @@ void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) { CopyPool::get
 
 // Page-locked arenas outlive their writer: a commit creates a fresh UnorderedWriter, and
 // page-locking 1 GB for every fileset of every commit (hipHostMalloc) costs more than the Put
-// copies themselves.  Process-wide pool, at most PFSCDC_UW_ARENA_POOL arenas (default 40:
-// one 32 GiB group's worth, so a group never page-locks fresh arenas; with 16 a 32 GiB group
-// re-allocated 18 of them every commit, 11.7 vs 27.8 GiB/s, profiles/r3/uw_groups/).
+// copies themselves.  Process-wide pool, capped by BYTES (each pooled arena holds its host
+// bytes page-locked and, with the device mirror, as many bytes of HBM):
+// PFSCDC_UW_ARENA_POOL_BYTES, default 40e9 (one 32 GiB group's worth of 1e9-byte arenas, so a
+// group never page-locks fresh ones; a 16-arena pool re-allocated 18 of them every commit,
+// 11.7 vs 27.8 GiB/s, profiles/r3/uw_groups/).  PFSCDC_UW_ARENA_POOL (a count of 1e9-byte
+// arenas) is still read when the byte form is unset.  pfscdc_uw_trim_cache() frees the pool.
 struct ArenaPool {
   std::mutex mu;
   std::vector<std::unique_ptr<Arena>> free;
-  size_t cap = [] {
-    const char* e = getenv("PFSCDC_UW_ARENA_POOL");
-    return e ? (size_t)std::max(0, atoi(e)) : (size_t)40;
+  uint64_t held = 0;  // bytes of the pooled arenas (host; the mirrors hold as many on devices)
+  uint64_t cap_bytes = []() -> uint64_t {
+    if (const char* e = getenv("PFSCDC_UW_ARENA_POOL_BYTES")) return (uint64_t)std::max(0LL, atoll(e));
+    if (const char* e = getenv("PFSCDC_UW_ARENA_POOL"))
+      return (uint64_t)std::max(0, atoi(e)) * 1000000000ull;
+    return 40000000000ull;
   }();
   std::unique_ptr<Arena> take(uint64_t bytes, int device) {
     std::lock_guard<std::mutex> lk(mu);
@@ -639,14 +660,38 @@ struct ArenaPool {
       if (free[i]->cap == bytes && free[i]->device == device) {
         std::unique_ptr<Arena> a = std::move(free[i]);
         free.erase(free.begin() + (ptrdiff_t)i);
+        held -= a->cap;
         a->used = 0;
         return a;
       }
     return nullptr;
   }
   void give(std::unique_ptr<Arena> a) {
-    std::lock_guard<std::mutex> lk(mu);
-    if (free.size() < cap) free.push_back(std::move(a));
+    std::unique_lock<std::mutex> lk(mu);
+    if (held + a->cap <= cap_bytes) {
+      held += a->cap;
+      free.push_back(std::move(a));
+      return;
+    }
+    lk.unlock();
+    a.reset();  // over the cap: page-locked host bytes and the mirror freed now
+  }
+  // Free the pooled arenas of one device (their mirrors live there; -1: every arena).
+  uint64_t trim(int device) {
+    std::vector<std::unique_ptr<Arena>> out;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = free.size(); i-- > 0;)
+        if (device < 0 || free[i]->device == device || free[i]->device < 0) {
+          held -= free[i]->cap;
+          out.push_back(std::move(free[i]));
+          free.erase(free.begin() + (ptrdiff_t)i);
+        }
+    }
+    uint64_t n = 0;
+    for (auto& a : out) n += a->cap;
+    out.clear();  // hipHostFree / hipFree outside the lock
+    return n;
   }
 };
 ArenaPool& arena_pool() {
@@ -1025,6 +1070,20 @@ int pfscdc_uw_timings(const pfscdc_uwriter* w, double out[9]) {
   for (const auto& g : w->workers)
     for (int k = 0; k < 8; k++) out[1 + k] += g->stage_ms[k];
   return PFSCDC_OK;
+}
+
+int pfscdc_uw_trim_cache(int device, uint64_t* arena_bytes_freed, uint32_t* ctxs_destroyed) {
+  const uint64_t b = arena_pool().trim(device);
+  const uint32_t n = ctx_cache().trim(device);
+  if (arena_bytes_freed) *arena_bytes_freed = b;
+  if (ctxs_destroyed) *ctxs_destroyed = n;
+  return PFSCDC_OK;
+}
+
+uint64_t pfscdc_uw_cached_arena_bytes(void) {
+  ArenaPool& p = arena_pool();
+  std::lock_guard<std::mutex> lk(p.mu);
+  return p.held;
 }
 
 const char* pfscdc_uw_last_error(const pfscdc_uwriter* w) {

@@ -1095,6 +1095,10 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
     sbeg[s] = c->h_offs.p[g.file] + g.offset;
     ssz[s] = g.size;
   }
+  // the record set-up below overwrites h_segs/h_offs (and in place, the caller's bytes): a
+  // retry after any error from here on must be refused, not run on the overwritten arrays
+  c->scan_valid = false;
+  c->nsegs = 0;
   if (refs) {
     // a ciphertext buffer both chunk sets write (in place: the plaintext itself)
     uint8_t* ct = in_place ? const_cast<uint8_t*>(data) : nullptr;
@@ -1637,7 +1641,11 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   // a plain BLAKE2b pass over the ciphertext when they do not, so the serial chain of the
   // longest chunk carries only BLAKE2b (about half the per-block latency).
   uint8_t* ct = ctext_out;
-  bool split = refid_split(nr, c->num_cus);
+  // the ciphertext over the plaintext (PFSCDC_OPT_CTEXT_IN_PLACE) always takes the split form:
+  // the fused kernel reads its plaintext and writes its ciphertext through two __restrict__
+  // pointers, which must not alias (PFSCDC_REFID_SPLIT=0 cannot force it here)
+  const bool in_place = ct != nullptr && ct == data;
+  bool split = in_place || refid_split(nr, c->num_cus);
   if (split && !ct) {
     // a ciphertext copy of the whole input, only with room to spare (the fused pass needs
     // none, and other contexts on the device need theirs)

@@ -129,6 +129,76 @@ def gather_records(recs: np.ndarray, device=None, group=None) -> np.ndarray:
     return np.concatenate(parts) if parts else recs[:0]
 
 
+def gather_records_to_root(recs: np.ndarray, device=None, group=None, dst: int = 0,
+                           stats: Optional[dict] = None) -> Optional[np.ndarray]:
+    """Gather a variable number of fixed-size records per rank to rank ``dst`` alone, in rank
+    order: one all-gather of the 8-byte counts, then point-to-point sends of exactly each
+    rank's live records (RCCL send/recv over xGMI on device tensors, gloo on host tensors).
+    This is the chunk-ref index's collection point: one consumer, as fileset.Writer's
+    callback collects the DataRefs of every chunk in one place
+    (/root/reference/src/internal/storage/fileset/writer.go:127-149).  Nothing is padded and
+    no other rank receives anything.  Returns the records on ``dst``, None elsewhere;
+    ``stats`` (if given) gets the record count and the bytes ``dst`` received."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    recs = np.ascontiguousarray(recs)
+    isz = recs.dtype.itemsize
+    cnt = torch.tensor([len(recs)], dtype=torch.int64, device=device)
+    cnts = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(cnts, cnt, group=group)
+    cnts = cnts.cpu().numpy()
+
+    def peer(r):
+        return r if group is None else dist.get_global_rank(group, r)
+
+    if rank != dst:
+        if len(recs):
+            t = torch.from_numpy(recs.view(np.uint8).reshape(-1))
+            if device is not None:
+                t = t.to(device)
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, peer(dst), group)]):
+                req.wait()
+        return None
+    others = int(cnts.sum()) - len(recs)
+    buf = torch.empty(others * isz, dtype=torch.uint8, device=device)
+    ops, views, pos = [], {}, 0
+    for r in range(world):
+        n = int(cnts[r]) * isz
+        if r == dst or n == 0:
+            continue
+        views[r] = (pos, n)
+        ops.append(dist.P2POp(dist.irecv, buf[pos:pos + n], peer(r), group))
+        pos += n
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    got = buf.cpu().numpy() if others else np.zeros(0, dtype=np.uint8)
+    parts = []
+    for r in range(world):
+        if r == dst:
+            parts.append(recs)
+        elif r in views:
+            a, n = views[r]
+            parts.append(got[a:a + n].view(recs.dtype))
+    if stats is not None:
+        stats.update({"records": int(cnts.sum()), "bytes_received": others * isz,
+                      "count_bytes": 8 * world})
+    return np.concatenate(parts) if parts else recs[:0]
+
+
+def gather_index_to_root(segments: np.ndarray, file_base: int = 0, device=None, group=None,
+                         dst: int = 0, stats: Optional[dict] = None) -> Optional[np.ndarray]:
+    """The chunk-ref index (segment records with global file ids) of every rank on ``dst``
+    only, live records alone (gather_records_to_root); None on the other ranks."""
+    segs = np.ascontiguousarray(segments).copy()
+    if file_base:
+        segs["file"] = (segs["file"].astype(np.uint64) + np.uint64(file_base)).astype(np.uint32)
+    return gather_records_to_root(segs, device, group, dst, stats)
+
+
 def gather_blobs(blobs: Sequence[bytes], device=None, group=None) -> list[bytes]:
     """All-gather each rank's list of byte strings (encoded index roots and the like);
     returns every rank's blobs in rank order."""

@@ -71,6 +71,22 @@ class Storage:
         if c.ctx:  # (a context closed by its own finalizer is not reused)
             self._idle.append(c)
 
+    def trim(self) -> dict:
+        """Free what closed writers left for the next one: this Storage's idle data contexts
+        (stream, events, grow-only device staging) and, process-wide for this device, the
+        pooled page-locked fileset arenas with their device mirrors and the cached index
+        contexts (pfscdc_uw_trim_cache).  Call it with no writer open on this device."""
+        lib = _lib.load()
+        n_idle = len(self._idle)
+        while self._idle:
+            self._idle.pop().close()
+        freed, ctxs = C.c_uint64(0), C.c_uint32(0)
+        rc = lib.pfscdc_uw_trim_cache(self.device, C.byref(freed), C.byref(ctxs))
+        if rc != 0:
+            raise _lib.PfsCdcError(rc, "pfscdc_uw_trim_cache")
+        return {"data_contexts": n_idle, "arena_bytes": int(freed.value),
+                "cached_contexts": int(ctxs.value)}
+
 
 class UnorderedWriter:
     def __init__(self, storage: Storage):

@@ -99,6 +99,66 @@ def test_gather_index_equals_single_process(world):
         assert np.array_equal(got[f], want[f]), f
 
 
+def _files_rank_root(rank, world):
+    """The bench's per-step gather: live records to rank 0 only (counts first)."""
+    lens, offs, data = _workload()
+    b, e = pd.shard_files(lens, world)[rank]
+    if rank == world - 1:
+        e = b  # a rank with no records at all sends nothing
+    loffs = offs[b:e + 1] - offs[b]
+    ldata = data[int(offs[b]):int(offs[e])]
+    segs, _ = coracle.segment_files(ldata, loffs, P)
+    st = {}
+    got = pd.gather_index_to_root(segs, b, stats=st)
+    if rank != 0:
+        assert got is None and not st
+        return None
+    return got.tobytes(), st, (b, e)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_index_to_root_moves_live_records_only(world):
+    from pfs_amd import _lib
+
+    raw, st, _ = _spawn(_files_rank_root, world)
+    got = np.frombuffer(raw, dtype=_lib.segment_dtype())
+    lens, offs, data = _workload()
+    last_b = pd.shard_files(lens, world)[world - 1][0]  # the last rank's files are dropped
+    want, _ = coracle.segment_files(data[:int(offs[last_b])], offs[:last_b + 1], P)
+    assert len(got) == len(want) == st["records"]
+    for f in ("offset", "size", "file", "flags", "hash"):
+        assert np.array_equal(got[f], want[f]), f
+    # rank 0 received exactly the other ranks' live records, no padding
+    r0 = pd.shard_files(lens, world)[0]
+    own, _ = coracle.segment_files(data[:int(offs[r0[1]])], offs[:r0[1] + 1], P)
+    assert st["bytes_received"] == (len(want) - len(own)) * _lib.segment_dtype().itemsize
+
+
+def _records_root(rank, world):
+    recs = np.arange(rank * 3, dtype=np.int64) + 100 * rank  # rank 0: none
+    out = pd.gather_records_to_root(recs, dst=world - 1)
+    return out if rank == world - 1 else None
+
+
+def test_gather_records_to_other_root():
+    # the root need not be rank 0 (the helper's dst), and rank 0 may hold nothing
+    got = _spawn(_records_root_via0, 3)
+    want = np.concatenate([np.arange(r * 3, dtype=np.int64) + 100 * r for r in range(3)])
+    assert np.array_equal(got, want)
+
+
+def _records_root_via0(rank, world):
+    import torch.distributed as dist
+    out = _records_root(rank, world)
+    # hand rank 2's result to rank 0 (the spawn helper returns rank 0's value)
+    blob = torch.from_numpy(out if out is not None else np.zeros(0, np.int64))
+    n = torch.tensor([blob.numel()])
+    dist.broadcast(n, src=world - 1)
+    buf = blob if rank == world - 1 else torch.empty(int(n.item()), dtype=torch.int64)
+    dist.broadcast(buf, src=world - 1)
+    return buf.numpy()
+
+
 def test_shard_files_balanced_and_contiguous():
     rng = np.random.default_rng(0)
     sizes = rng.integers(0, 10_000_000, 1000)

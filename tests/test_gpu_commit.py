@@ -215,3 +215,44 @@ def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkey
         chunk = host[int(coffs[i]):int(coffs[i + 1])].tobytes()
         rid, dek = Ch.create_ref_id(chunk)
         assert bytes(refs0[i]["id"]) == rid and bytes(refs0[i]["dek"]) == dek
+
+
+@pytest.mark.parametrize("refid_split", ["0", "1"])
+def test_ciphertext_in_place_whatever_the_refid_form(refid_split, monkeypatch):
+    """In place, chunk.Create always takes the split Ref.Id form: the fused kernel's plaintext
+    and ciphertext pointers are __restrict__ and must not alias, so PFSCDC_REFID_SPLIT=0 (or a
+    chunk count above the quads, which picks the fused form) must not reach it with
+    ctext_out == data.  Refs and the buffer equal the copy form's."""
+    import torch
+
+    p = Ch.Params(average_bits=13, seed=1, min=4000, max=60000)
+    rng = np.random.default_rng(23)
+    lens = np.concatenate([rng.integers(0, 9000, 150), rng.integers(20_000, 150_000, 25)])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    host = synthetic_bytes(offs, 23)
+    streams = [0, len(lens) // 2, len(lens)]
+    cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+    monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "0")
+
+    def run(in_place, split_env):
+        if split_env is None:
+            monkeypatch.delenv("PFSCDC_REFID_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("PFSCDC_REFID_SPLIT", split_env)
+        c = Chunker(cp, 0)
+        c.set_cuts_only(True)
+        c.set_ctext_in_place(in_place)
+        t = torch.from_numpy(host).to("cuda:0")
+        c.scan(t, offs)
+        coffs, _, known = c.form_chunks(streams)
+        refs, chash, seg = c.commit_refs(t, coffs, known)
+        c.close()
+        return coffs, refs, chash, seg, t.cpu().numpy()
+
+    coffs, refs0, chash0, seg0, _ = run(False, None)
+    _, refs, chash, seg, ct = run(True, refid_split)
+    assert np.array_equal(refs["id"], refs0["id"]) and np.array_equal(refs["dek"], refs0["dek"])
+    assert np.array_equal(chash, chash0) and np.array_equal(seg, seg0)
+    for i in range(len(coffs) - 1):
+        c = ct[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        assert hashlib.blake2b(c, digest_size=32).digest() == bytes(refs[i]["id"]), i

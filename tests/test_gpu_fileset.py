@@ -171,3 +171,23 @@ def test_large_puts_copy_pool_reference_params(workers, monkeypatch):
     want, got, wlog, glog = run_both(ops, Ch.Params(), 10_000_000)
     assert len(want) == 5
     check(want, got, wlog, glog)
+
+
+def test_trim_cache_frees_pooled_arenas_and_writers_still_agree():
+    """the arenas (page-locked host bytes + device mirrors) and contexts a destroyed
+    writer leaves for the next one are freed by Storage.trim / pfscdc_uw_trim_cache, and a
+    writer made after a trim allocates afresh and still equals the restated reference."""
+    lib = _lib.load()
+    ops, _ = workload(5, 60, 40_000)
+    st = PF.Storage(0, cp(SMALL), 400_000, cp(SMALL_INDEX))
+    pw = st.new_unordered_writer()
+    for op in ops:
+        (pw.put if op[0] == "put" else pw.delete)(*op[1:])
+    pw.close()
+    pw.release()
+    assert lib.pfscdc_uw_cached_arena_bytes() > 0  # the written filesets' arenas were pooled
+    out = st.trim()
+    assert out["data_contexts"] >= 1 and out["arena_bytes"] > 0
+    assert lib.pfscdc_uw_cached_arena_bytes() == 0
+    want, got, wlog, glog = run_both(ops, SMALL, 400_000, SMALL_INDEX)
+    check(want, got, wlog, glog)
