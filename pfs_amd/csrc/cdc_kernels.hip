@@ -325,6 +325,71 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
       record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec);        \
   }
 
+// --- the pair form of the g-recurrence (PAIR, narrow masks): two positions per 64-bit rotation --
+// g_{t+1} = rotl(g_{t-1}, 2) ^ rotl(T[x_t], 1) ^ T[x_{t+1}], so with 16-byte table entries
+// {T, R = rotl(T, 1)} (16 copies, entry idx of copy c at idx * 256 + c * 16: every 16-lane group
+// of a ds_read_b128 conflict free with c = lane & 15) a pair of positions costs one 64-bit
+// rotation by 2 (two v_alignbit_b32) and only the low word of the intermediate g_t (one
+// v_alignbit_b32): 11 VALU per pair (2 v_perm_b32 addresses, 3 v_alignbit_b32, 2 v_bitop3_b32
+// XOR3s for the keys' inputs, 2 XORs, 1 XOR3 for the high word, 1 v_min3_u32) instead of 13.
+// The even position reads its whole entry (ds_read_b128), the odd one T alone (ds_read_b64 at
+// the same 16-copy layout: lanes l and l + 16 share a copy, 2-way on that read).  16 copies of
+// 16 B = the same 64 KiB of LDS as the one-position form's 32 copies of 8 B.
+#ifndef PFS_EXP_PAHEAD
+#define PFS_EXP_PAHEAD 5
+#endif
+constexpr bool kScanPairDefault = false;  // A/B until measured
+constexpr int kPAhead = PFS_EXP_PAHEAD;  // pairs of lookups in flight (two ds_reads each)
+static_assert(kPAhead >= 1 && 2 * kPAhead - 1 <= 15, "lgkmcnt is 4 bits");
+
+PFS_DEV u32x4 lds_read_b128_async(uint32_t a) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+#define PFS_ROLL64P(IN, POS)                                                              \
+  {                                                                                       \
+    uint32_t acc = 0xffffffffu;                                                           \
+    u32x4 ea_[kPAhead];                                                                   \
+    uint64_t eb_[kPAhead];                                                                \
+    StaticFor<0, kPAhead>::run([&](auto pc) {                                             \
+      constexpr int t = 2 * decltype(pc)::value;                                          \
+      ea_[t / 2] = lds_read_b128_async(tab_addr(IN[t >> 2], lane_off, t & 3));            \
+      eb_[t / 2] = lds_read_async(tab_addr(IN[(t + 1) >> 2], lane_off, (t + 1) & 3));     \
+    });                                                                                   \
+    StaticFor<0, 32>::run([&](auto pc) {                                                  \
+      constexpr int p = decltype(pc)::value, t = 2 * p;                                   \
+      /* pairs in flight: p .. min(p+K-1, 31); wait until only the younger ones remain */  \
+      constexpr int inflight = (32 - p < kPAhead) ? 32 - p : kPAhead;                     \
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (inflight - 1)) << 8));                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      const u32x4 a_ = ea_[p % kPAhead];                                                  \
+      const uint64_t b_ = eb_[p % kPAhead];                                               \
+      const uint32_t l0_ = __builtin_amdgcn_alignbit(hl, hh, 31);                         \
+      const uint32_t k0_ = xor3(l0_, a_.x, ring[t]);                                      \
+      ring[t] = l0_ ^ a_.x;                                                               \
+      asm volatile("" : "+v"(ring[t])); /* computed now: frees l0_ and the entry */       \
+      const uint32_t r2l_ = __builtin_amdgcn_alignbit(hl, hh, 30);                        \
+      const uint32_t r2h_ = __builtin_amdgcn_alignbit(hh, hl, 30);                        \
+      const uint32_t n1_ = xor3(r2l_, a_.z, (uint32_t)b_);                                \
+      const uint32_t k1_ = n1_ ^ ring[t + 1];                                             \
+      ring[t + 1] = n1_;                                                                  \
+      hl = n1_;                                                                           \
+      hh = xor3(r2h_, a_.w, (uint32_t)(b_ >> 32));                                        \
+      acc = acc < k0_ ? acc : k0_; /* one v_min3_u32 with the next line */                \
+      acc = acc < k1_ ? acc : k1_;                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr (p + kPAhead < 32) {                                                   \
+        constexpr int u = t + 2 * kPAhead;                                                \
+        ea_[p % kPAhead] = lds_read_b128_async(tab_addr(IN[u >> 2], lane_off, u & 3));    \
+        eb_[p % kPAhead] = lds_read_async(tab_addr(IN[(u + 1) >> 2], lane_off, (u + 1) & 3)); \
+      }                                                                                   \
+    });                                                                                   \
+    if (__builtin_expect(acc < cand_thr, 0))                                              \
+      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec);        \
+  }
+
 // Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
 // them 128 bytes at a time.  Per step, 8 LDS-DMA instructions (global_load_lds_dwordx4)
 // each fetch one full 128-byte line from 8 strips (8 lines per instruction: the coalesced
@@ -362,7 +427,7 @@ PFS_DEV void span_end(uint64_t* span, SpanClock c) {
   }
 }
 
-template <bool WIDE>
+template <bool WIDE, bool PAIR>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
@@ -375,17 +440,29 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t n_main = n & ~63ULL;
 
-  // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
-  for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
-    const int idx = i >> 5, c = i & 31;
-    // narrow masks roll in a frame rotated left by kshift = 32 - bits (see PFS_ROLL64G)
-    const uint64_t v = table[idx];
-    reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
-        WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
+  if constexpr (PAIR) {
+    // {T, rotl(T, 1)} replicated: entry idx of copy c at byte idx*256 + c*16 (PFS_ROLL64P)
+    for (int i = threadIdx.x; i < 256 * 16; i += kScanBlock) {
+      const int idx = i >> 4, c = i & 15;
+      const uint64_t t0 = table[idx];
+      const uint64_t v = kshift == 0 ? t0 : (t0 << kshift) | (t0 >> (64 - kshift));
+      uint64_t* e = reinterpret_cast<uint64_t*>(smem + idx * 256 + c * 16);
+      e[0] = v;
+      e[1] = rotl1_64(v);
+    }
+  } else {
+    // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
+    for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
+      const int idx = i >> 5, c = i & 31;
+      // narrow masks roll in a frame rotated left by kshift = 32 - bits (see PFS_ROLL64G)
+      const uint64_t v = table[idx];
+      reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
+          WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
+    }
   }
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t lane_off = (lane & 31u) * 8u;
+  const uint32_t lane_off = PAIR ? (lane & 15u) * 16u : (lane & 31u) * 8u;
   uint8_t* wbuf = smem + kTableLdsBytes + wave * kStageBytes;
   const uint32_t rd_base = lane * 128u;
   const uint32_t swz_l = stage_swz(lane);
@@ -498,6 +575,9 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
           if constexpr (WIDE) {
             PFS_ROLL64(c0, prv, pos)
             if (pos + 64 < n) PFS_ROLL64(c1, c0, pos + 64)
+          } else if constexpr (PAIR) {
+            PFS_ROLL64P(c0, pos)
+            if (pos + 64 < n) PFS_ROLL64P(c1, pos + 64)
           } else {
             PFS_ROLL64G(c0, pos)
             if (pos + 64 < n) PFS_ROLL64G(c1, pos + 64)
@@ -1483,7 +1563,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // other alone at the lone-wave rate.  At least every fair_every blocks each wave adds the
   // blocks it ran to a launch-wide counter and raises its issue priority while it is behind
   // the launch's average, so the waves of a SIMD advance together.
-  const uint32_t kFairEvery = fair_every ? fair_every : 256;
+  const uint32_t kFairEvery = (fair_every & 0x7fffffffu) ? (fair_every & 0x7fffffffu) : 256;
+  const bool fair_graded = (fair_every >> 31) != 0;
   uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; fair share, the trace)
   uint32_t reported = 0;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kHashBlock / 64);
@@ -1569,7 +1650,9 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         tot = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tot >> 32)) << 32) |
               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tot);
         reported = wave_steps;
-        if ((uint64_t)wave_steps * nwaves < tot + d) __builtin_amdgcn_s_setprio(1);
+        const uint64_t mine = (uint64_t)wave_steps * nwaves, all = tot + d;
+        if (fair_graded && mine + 2ull * kFairEvery * nwaves < all) __builtin_amdgcn_s_setprio(2);
+        else if (mine < all) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       } else if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
         const uint64_t T = prio_blocks & 0x3fffffffu, rem = active ? nblk - blk : 0;
@@ -2054,11 +2137,21 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
 // on the ctx's device before any launch; idempotent, so every ctx sets them on its device.
 hipError_t prepare_kernels() {
   const int lds = (int)kScanLdsBytes;
-  hipError_t e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false>,
+  hipError_t e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)cdc_scan_kernel<true>,
+  return hipFuncSetAttribute((const void*)cdc_scan_kernel<true, false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+// The narrow scan's form: one position per rotation (PFS_ROLL64G, 32 copies of T) or pairs
+// (PFS_ROLL64P, 16 copies of {T, rotl(T, 1)}).  PFSCDC_SCAN_PAIR=0/1, read per launch.
+static bool scan_pair() {
+  const char* e = getenv("PFSCDC_SCAN_PAIR");
+  return e && *e ? atoi(e) != 0 : kScanPairDefault;
 }
 
 hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
@@ -2076,14 +2169,18 @@ hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, con
                        uint64_t* n_entries, uint64_t* span, hipStream_t st, const uint32_t* skip) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
-  if (average_bits <= 32)
-    cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 32 - average_bits,
-                                                          mask64, ntiles, recs, unit_ctr, done_ctr,
-                                                          entries, n_entries, skip, span);
+  if (average_bits <= 32 && scan_pair())
+    cdc_scan_kernel<false, true><<<grid, kScanBlock, lds, st>>>(
+        data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
+        entries, n_entries, skip, span);
+  else if (average_bits <= 32)
+    cdc_scan_kernel<false, false><<<grid, kScanBlock, lds, st>>>(
+        data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
+        entries, n_entries, skip, span);
   else
-    cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(data, tail, n, d_table, 64 - average_bits,
-                                                         mask64, ntiles, recs, unit_ctr, done_ctr,
-                                                         entries, n_entries, skip, span);
+    cdc_scan_kernel<true, false><<<grid, kScanBlock, lds, st>>>(
+        data, tail, n, d_table, 64 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
+        entries, n_entries, skip, span);
   return hipGetLastError();
 }
 
@@ -2139,14 +2236,14 @@ static uint32_t hash_prio_blocks() {
   return v;
 }
 
-// PFSCDC_HASH_FAIR_EVERY: blocks between a fair-share wave's priority updates (default 256)
+// PFSCDC_HASH_FAIR_EVERY: blocks between a fair-share wave's priority updates (default 256);
+// PFSCDC_HASH_FAIR_GRADED=1: priority 2 for a wave more than two intervals behind the launch
+// average, 1 behind it, 0 ahead (bit 31 of the kernel argument).  Read per launch.
 static uint32_t hash_fair_every() {
-  static const uint32_t v = [] {
-    const char* e = getenv("PFSCDC_HASH_FAIR_EVERY");
-    const int x = e ? atoi(e) : 0;
-    return (uint32_t)(x >= 8 && x <= 65536 ? x : 256);
-  }();
-  return v;
+  const char* e = getenv("PFSCDC_HASH_FAIR_EVERY");
+  const int x = e ? atoi(e) : 0;
+  const char* g = getenv("PFSCDC_HASH_FAIR_GRADED");
+  return (uint32_t)(x >= 8 && x <= 65536 ? x : 256) | (g && atoi(g) ? 0x80000000u : 0u);
 }
 
 // Waves per SIMD for a hash launch.  One quad runs a chain's 128-B blocks strictly in order,

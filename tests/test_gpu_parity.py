@@ -267,7 +267,7 @@ def test_kernel_spans_and_clocks_are_recorded():
     c.close()
 
 
-@pytest.mark.parametrize("waves", ["1", "2"])
+@pytest.mark.parametrize("waves", ["1", "2", "2g"])
 @pytest.mark.parametrize("bin_bytes", ["0", "60000", "1000000000000"])
 @pytest.mark.parametrize("ref_ids", [False, True])
 def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
@@ -275,9 +275,13 @@ def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
     lpt_order_block): digests, and with PFSCDC_OPT_REF_IDS the per-segment Ref.Ids, equal to
     the oracle whether no file, some files or every file forms a bin (empty files and files
     cut into many segments included); at two waves per SIMD the hash launch also runs the
-    fair-share issue priority (its launch-wide counter and the capped quiet countdown)."""
+    fair-share issue priority (its launch-wide counter and the capped quiet countdown); "2g":
+    the graded fair share (PFSCDC_HASH_FAIR_GRADED) with a short interval."""
     monkeypatch.setenv("PFSCDC_HASH_BIN_BYTES", bin_bytes)
-    monkeypatch.setenv("PFSCDC_HASH_WAVES", waves)
+    monkeypatch.setenv("PFSCDC_HASH_WAVES", waves[0])
+    if waves == "2g":
+        monkeypatch.setenv("PFSCDC_HASH_FAIR_GRADED", "1")
+        monkeypatch.setenv("PFSCDC_HASH_FAIR_EVERY", "16")
     rng = np.random.default_rng(5)
     lens = np.concatenate([rng.integers(0, 70_000, 200), [0, 0, 1, 30_000, 250_000, 0]])
     rng.shuffle(lens)
@@ -294,3 +298,28 @@ def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
             rid, dek = Ch.create_ref_id(data[a:a + int(g["size"])].tobytes())
             assert bytes(refs[i]["dek"]) == dek and bytes(refs[i]["id"]) == rid, i
     c.close()
+
+
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_scan_forms_equal_oracle(form, monkeypatch):
+    """Both forms of the narrow scan: one position per 64-bit rotation (32 copies of T) and
+    pairs of positions per rotation by 2 (16 copies of {T, rotl(T, 1)}, PFSCDC_SCAN_PAIR=1):
+    every mask width, edge sizes, dense tiles, periodic data and the reference parameters."""
+    monkeypatch.setenv("PFSCDC_SCAN_PAIR", form)
+    for bits in (1, 4, 9, 20, 23, 31, 32):
+        p = Ch.Params(average_bits=bits, seed=bits % 3, min=100, max=4000)
+        offs = np.array([0, 70_000, 70_001, 200_000, 263_000], dtype=np.uint64)
+        data = synthetic_bytes(offs, 60 + bits)
+        assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+    lens = [0, 1, 63, 64, 65, 127, 128, 129, 1999, 2000, 2001, 29999, 30000, 30001, 0, 60001]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 6)
+    assert_same(chunker_for(SMALL).scan(data, offs), data, offs, SMALL)
+    p = Ch.Params(average_bits=10, seed=1, min=3000, max=40000)
+    pat = np.frombuffer(bytes(range(48)), dtype=np.uint8)
+    data = np.concatenate([np.tile(pat, 30_000), synthetic_bytes([0, 1 << 20], 8)])
+    offs = np.array([0, len(data) // 3, len(data)], dtype=np.uint64)
+    assert_same(chunker_for(p).scan(data, offs), data, offs, p)
+    offs = np.array([0, 3 << 20, (3 << 20) + 12345, (12 << 20) + 7, 22 << 20], dtype=np.uint64)
+    data = synthetic_bytes(offs, 12)
+    assert_same(chunker_for(DEFAULT).scan(data, offs), data, offs, DEFAULT)
