@@ -511,15 +511,18 @@ struct FilesetWriter {  // fileset/writer.go:21-182
   }
 
   int finish() {  // Close after the data writer closed: the last entry, then the indexes
-    int rc = PFSCDC_OK;
-    if (last_idx) {
-      rc = additive.write_index(last_idx, 0);
-      if (rc) return rc;
-    }
+    int rc = finish_last_entry();
     IndexT *a = nullptr, *d = nullptr;
-    rc = additive.close(&a);
+    if (!rc) rc = additive.close(&a);
     if (!rc) rc = deletive.close(&d);
     if (rc) return rc;
+    finish_info(a, d);
+    return PFSCDC_OK;
+  }
+  int finish_last_entry() {  // the additive index entry of the last file (writer.go:151-167)
+    return last_idx ? additive.write_index(last_idx, 0) : PFSCDC_OK;
+  }
+  void finish_info(IndexT* a, IndexT* d) {  // the roots of the closed indexes
     if (a) {
       info.has_additive = true;
       info.additive = enc_index(*a);
@@ -528,9 +531,47 @@ struct FilesetWriter {  // fileset/writer.go:21-182
       info.has_deletive = true;
       info.deletive = enc_index(*d);
     }
-    return PFSCDC_OK;
   }
 };
+
+// IndexWriter::close of many index writers (the additive and deletive indexes of every
+// fileset of a group), level by level: level k of every writer still open is closed in one
+// grouped close on the level's ctx (one scan, one hash launch and one chunk.Create instead of
+// one of each per writer), which runs their callbacks and so fills level k + 1.  Each index
+// stream is independent, so the roots and events equal closing the writers one by one; a
+// writer stops at the level that closed with one annotation in one chunk, as close() does.
+int close_indexes_grouped(const std::vector<IndexWriter*>& iws) {
+  std::vector<size_t> next(iws.size(), 0);
+  std::vector<char> done(iws.size(), 0);
+  for (IndexWriter* w : iws) w->closed = true;
+  for (;;) {
+    int lvl = -1;
+    for (size_t i = 0; i < iws.size(); i++) {
+      if (done[i]) continue;
+      if (next[i] >= iws[i]->levels.size()) {
+        done[i] = 1;
+        continue;
+      }
+      if (lvl < 0 || (int)next[i] < lvl) lvl = (int)next[i];
+    }
+    if (lvl < 0) break;
+    std::vector<size_t> ids;
+    std::vector<pfscdc_writer*> cws;
+    for (size_t i = 0; i < iws.size(); i++)
+      if (!done[i] && (int)next[i] == lvl) {
+        ids.push_back(i);
+        cws.push_back(iws[i]->levels[lvl]->cw);
+      }
+    int rc = pfscdc::writers_close_group(cws.data(), cws.size(), nullptr, nullptr, 0);
+    if (rc) return rc;
+    for (size_t i : ids) {
+      pfscdc_writer* cw = iws[i]->levels[lvl]->cw;
+      if (pfscdc_writer_annotation_count(cw) == 1 && pfscdc_writer_chunk_count(cw) == 1) done[i] = 1;
+      else next[i]++;
+    }
+  }
+  return PFSCDC_OK;
+}
 
 // Host bytes of one fileset's Puts, appended in arrival order (a Put copies into it once);
 // the Buffer keeps each file as spans of it and the fileset's chunk writer uploads the spans
@@ -734,6 +775,11 @@ struct GroupWorker {
   double stage_ms[8] = {};  // close_group's 6 stages, [6] the index writers, [7] group wall
 };
 
+static bool index_grouped() {
+  const char* e = getenv("PFSCDC_UW_INDEX_GROUPED");
+  return !(e && *e && atoi(e) == 0);
+}
+
 struct pfscdc_uwriter {  // unordered_writer.go:15-26
   int64_t mem_threshold = 1000000000;
   int64_t mem_available = 1000000000;
@@ -869,14 +915,26 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     if (!rc)
       rc = pfscdc::writers_close_group(cws.data(), cws.size(), gw.stage_ms, evs.data(), evs.size());
     const auto g1 = clk::now();
-    for (size_t i = 0; i < fws.size() && !rc; i++) {
-      rc = fws[i]->finish();
-      if (!rc) {
-        std::lock_guard<std::mutex> lk(fs_mu);
-        const size_t k = fs0 + i;
-        if (filesets.size() <= k) filesets.resize(k + 1);
-        filesets[k] = std::move(fws[i]->info);
+    // the indexes of every fileset of the group, closed level by level in grouped closes
+    // (PFSCDC_UW_INDEX_GROUPED=0: one fileset at a time, A/B)
+    if (index_grouped()) {
+      std::vector<IndexWriter*> iws;
+      for (size_t i = 0; i < fws.size() && !rc; i++) {
+        rc = fws[i]->finish_last_entry();
+        iws.push_back(&fws[i]->additive);
+        iws.push_back(&fws[i]->deletive);
       }
+      if (!rc) rc = close_indexes_grouped(iws);
+      for (size_t i = 0; i < fws.size() && !rc; i++)
+        fws[i]->finish_info(fws[i]->additive.root, fws[i]->deletive.root);
+    } else {
+      for (size_t i = 0; i < fws.size() && !rc; i++) rc = fws[i]->finish();
+    }
+    for (size_t i = 0; i < fws.size() && !rc; i++) {
+      std::lock_guard<std::mutex> lk(fs_mu);
+      const size_t k = fs0 + i;
+      if (filesets.size() <= k) filesets.resize(k + 1);
+      filesets[k] = std::move(fws[i]->info);
     }
     fws.clear();
     const auto g2 = clk::now();

@@ -172,6 +172,10 @@ idx = pd.gather_index(res.segments, 0, pd.max_segments(np.diff(offs), p.min), de
 want, _ = coracle.segment_files(data, offs, p)
 assert idx.tobytes() == want.tobytes()
 assert pd.gather_records(want, device=dev).tobytes() == want.tobytes()
+st = {}
+assert pd.gather_index_to_root(res.segments, device=dev, stats=st).tobytes() == want.tobytes()
+assert st == {"records": len(want), "bytes_received": 0, "count_bytes": 8}
+assert pd.gather_records_to_root(want, device=dev).tobytes() == want.tobytes()
 assert pd.gather_blobs([b"abc", b"", b"xyz"], device=dev) == [b"abc", b"", b"xyz"]
 n = 3_000_000
 s = synthetic_bytes([0, n], 0xC3)

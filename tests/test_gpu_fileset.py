@@ -88,10 +88,14 @@ def workload(seed, nfiles, max_len, dirs=4):
     return ops, data
 
 
+@pytest.mark.parametrize("index_grouped", ["1", "0"])
 @pytest.mark.parametrize("inflight", [None, "300000"])
-def test_unordered_writer_many_filesets_multilevel_index(inflight, monkeypatch):
+def test_unordered_writer_many_filesets_multilevel_index(inflight, index_grouped, monkeypatch):
     # inflight: serialized filesets are written in groups of up to this many bytes (the
-    # default holds all of them until Close); the output must not depend on the grouping
+    # default holds all of them until Close); the output must not depend on the grouping.
+    # index_grouped: a group's index writers closed level by level in grouped closes (the
+    # default) or one fileset at a time
+    monkeypatch.setenv("PFSCDC_UW_INDEX_GROUPED", index_grouped)
     if inflight:
         monkeypatch.setenv("PFSCDC_UW_INFLIGHT", inflight)
     ops, _ = workload(1, 160, 40_000)
