@@ -364,6 +364,9 @@ PFS_DEV u32x4 lds_read_b128_async(uint32_t a) {
       constexpr int inflight = (32 - p < kPAhead) ? 32 - p : kPAhead;                     \
       __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (inflight - 1)) << 8));                   \
       __builtin_amdgcn_sched_barrier(0);                                                  \
+      /* all four words stay allocated until the read retires (T_hi is unused: left to */ \
+      /* itself the compiler reuses its register while the ds_read_b128 is in flight) */  \
+      asm volatile("" : "+v"(ea_[p % kPAhead]));                                          \
       const u32x4 a_ = ea_[p % kPAhead];                                                  \
       const uint64_t b_ = eb_[p % kPAhead];                                               \
       const uint32_t l0_ = __builtin_amdgcn_alignbit(hl, hh, 31);                         \
