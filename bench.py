@@ -454,24 +454,32 @@ def main():
     last = {}
 
     def finish(k, record):
+        """Wait for context k's step; its records and timings (copies: the context can take
+        its next step at once)."""
         res = chunkers[k].wait()
         pending[k] = False
-        if gather:
-            segs = res.segments.copy()
-            segs["file"] = work.gid[segs["file"]].astype(np.uint32)
-            if world > 1:
-                # counts first, then each rank's live records point to point to rank 0
-                g0 = time.perf_counter()
-                last["index"] = pd.gather_index_to_root(segs, device=cdev, stats=gstats)
-                if record:
-                    gather_ms.append((time.perf_counter() - g0) * 1e3)
-            else:
-                last["index"] = segs
         if record:
             steps_t.append(chunkers[k].timings())
             done_at.append(time.perf_counter())
         last[k] = res
         return res
+
+    def gather_step(res, record):
+        """The step's chunk-ref index to rank 0.  Called after the next step is enqueued, so
+        the GPU has work queued while the host waits on the collective (whose kernels may
+        wait for CUs behind that step's scan)."""
+        if not gather:
+            return
+        segs = res.segments.copy()
+        segs["file"] = work.gid[segs["file"]].astype(np.uint32)
+        if world > 1:
+            # counts first, then each rank's live records point to point to rank 0
+            g0 = time.perf_counter()
+            last["index"] = pd.gather_index_to_root(segs, device=cdev, stats=gstats)
+            if record:
+                gather_ms.append((time.perf_counter() - g0) * 1e3)
+        else:
+            last["index"] = segs
 
     seq = [0]  # the context rotation continues across the warmup and timed runs: restarting
     # it at context 0 after an odd warmup left the two steps serialised on the GPU
@@ -480,16 +488,17 @@ def main():
         for _ in range(nsteps):
             k = seq[0] % NC
             seq[0] += 1
-            if pending[k]:
-                finish(k, record)
+            done = finish(k, record) if pending[k] else None
             if ahead:  # after everything the other context has enqueued (the previous step)
                 chunkers[k].wait_for(chunkers[(k + 1) % NC])
             chunkers[k].scan_async(batches[k % S], work.offs)
             pending[k] = True
+            if done is not None:
+                gather_step(done, record)
         for j in range(NC):  # drain in launch order
             kk = (seq[0] + j) % NC
             if pending[kk]:
-                finish(kk, record)
+                gather_step(finish(kk, record), record)
 
     run(args.warmup, False)
     if world > 1:
