@@ -1054,6 +1054,16 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
   for (int x = 0; x < 2; x++)
     if (hipEventElapsedTime(&ms, c->pev[0], X[x]->ev[6]) == hipSuccess) b = std::max(b, ms);
   drain.armed = false;  // create_refs_finish waited for both streams
+  if (getenv("PFSCDC_TRACE")) {  // each set's timeline (ms after the scan): hashes, chunk.Create
+    float t[4] = {0, 0, 0, 0};
+    for (int x = 0; x < 2; x++) {
+      (void)hipEventElapsedTime(&t[x], c->pev[0], c->pev[1 + x]);
+      (void)hipEventElapsedTime(&t[2 + x], c->pev[0], X[x]->ev[6]);
+    }
+    fprintf(stderr, "[pfscdc] commit two sets: long %zu chunks %zu segs: hashes %.1f create %.1f | "
+            "short %zu chunks %zu segs: hashes %.1f create %.1f ms\n", sel[0].size(),
+            rec_seg[0].size(), t[0], t[2], sel[1].size(), rec_seg[1].size(), t[1], t[3]);
+  }
   c->create_hash_ms = a;  // both sets' hashes (they overlap the long set's Ref.Id pass)
   c->create_ms = b;
   c->scan_valid = false;
