@@ -870,6 +870,17 @@ static int commit_long_create_waves() {  // PFSCDC_COMMIT_LONG_CREATE_WAVES (0: 
   const int x = e ? atoi(e) : 0;
   return x >= 1 && x <= 2 ? x : 0;
 }
+// PFSCDC_COMMIT_LONG_PRIO (default 1): the long set's hash launches raise their issue priority
+// (s_setprio 2 while a quad has a block left); 0: no priority.  PFSCDC_COMMIT_CHACHA_PRIO
+// (default 1): the long set's ChaCha20 pass likewise.  A/B knobs.
+static bool commit_long_prio() {
+  const char* e = getenv("PFSCDC_COMMIT_LONG_PRIO");
+  return !(e && *e && atoi(e) == 0);
+}
+static bool commit_chacha_prio() {
+  const char* e = getenv("PFSCDC_COMMIT_CHACHA_PRIO");
+  return !(e && *e && atoi(e) == 0);
+}
 static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
   const char* e = getenv("PFSCDC_COMMIT_SHORT_WAVES");
   const int x = e ? atoi(e) : 0;
@@ -997,7 +1008,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
                                u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
                                x ? std::min(w, commit_short_waves())
                                  : chains_only ? 1 : commit_long_waves() ? commit_long_waves() : w,
-                               x ? kNoPrio : 1u));
+                               x || !commit_long_prio() ? kNoPrio : 1u));
     if (R)
       HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
                                hipMemcpyDeviceToHost, st));
@@ -1023,8 +1034,8 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
         if (hash_known[i])
           std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * known_seg[i], 32);
       u->cr_wave_cap = x ? commit_short_waves() : commit_long_create_waves();
-      u->cr_hash_prio = x ? kNoPrio : 1u;
-      u->cr_chacha_prio = x == 0;
+      u->cr_hash_prio = x || !commit_long_prio() ? kNoPrio : 1u;
+      u->cr_chacha_prio = x == 0 && commit_chacha_prio();
       u->cr_one_stream = true;  // each set has one stream (two in all)
       if (x == 0 && chains_only) HIP_OK(c, hipStreamWaitEvent(c->stream, c->pev[2], 0));
       const int rc = create_refs_device(u, data, nbytes, co, nchunks, content_hashes, all.data(),
