@@ -1882,6 +1882,113 @@ __global__ __launch_bounds__(256) void chacha_xor_kernel(
     }
   }
 }
+// The same pass with coalesced memory traffic.  Above, lane l XORs its own 64-byte block, so
+// one 16-byte load or store instruction spans 64 blocks (4 KiB, 32 lines); here each lane
+// still computes its block's keystream, parks it in LDS (64 B per lane, 16-byte slots
+// XOR-rotated by (block >> 1) & 3 so the 8-lane groups of ds_write_b128 and the 16-lane
+// groups of ds_read_b128 are conflict-free), and the wave then walks its 64-block window as
+// 256 consecutive 16-byte pieces: lane l takes pieces l, l + 64, l + 128, l + 192, so one
+// instruction covers 1 KiB of one chunk (8 lines).  A chunk's last, partial block is written
+// byte by byte up to the chunk's end (in place, the next chunk's first block is another
+// lane's).  PFSCDC_CHACHA_COALESCED=0: the per-lane form (A/B).
+constexpr int kChachaBlock = 256;
+__global__ __launch_bounds__(kChachaBlock) void chacha_xor_coalesced_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
+    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
+  __shared__ __attribute__((aligned(16))) uint32_t s_ks[kChachaBlock / 64][64 * 16];
+  __shared__ uint64_t s_at[kChachaBlock / 64][64];
+  __shared__ int64_t s_avail[kChachaBlock / 64][64];
+  const uint64_t nblocks = blk_base[n];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  uint32_t* const ks = s_ks[wv];
+  const uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x +
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+  for (uint64_t g0 = w0; g0 < nblocks; g0 += stride) {
+    uint32_t lo = 0, hi = n;  // the last r with blk_base[r] <= g0
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (blk_base[mid] <= g0) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t g = g0 + lane;
+    uint32_t x[16];
+    uint64_t at = 0;
+    int64_t avail = 0;  // <= 0: no block here (past the pass's last block)
+    if (g < nblocks) {
+      while (blk_base[lo + 1] <= g) lo++;
+      const pfscdc_segment& sg = segs[lo];
+      const uint64_t b = g - blk_base[lo];
+      at = offs[sg.file] + sg.offset + 64 * b;
+      avail = (int64_t)(sg.size - 64 * b);
+      const uint4 k0 = reinterpret_cast<const uint4*>(refs[lo].dek)[0];
+      const uint4 k1 = reinterpret_cast<const uint4*>(refs[lo].dek)[1];
+      const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                              k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w,
+                              (uint32_t)b, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = s[i];
+#pragma unroll
+      for (int r = 0; r < 10; r++) {
+        PFS_CQR(0, 4, 8, 12);
+        PFS_CQR(1, 5, 9, 13);
+        PFS_CQR(2, 6, 10, 14);
+        PFS_CQR(3, 7, 11, 15);
+        PFS_CQR(0, 5, 10, 15);
+        PFS_CQR(1, 6, 11, 12);
+        PFS_CQR(2, 7, 8, 13);
+        PFS_CQR(3, 4, 9, 14);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] += s[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = 0;
+    }
+    // park the keystream: slot q of block `lane` at lane * 64 + 16 * ((q + (lane >> 1)) & 3)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t slot = ((uint32_t)q + (lane >> 1)) & 3u;
+      *reinterpret_cast<uint4*>(ks + lane * 16 + 4 * slot) =
+          make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    }
+    s_at[wv][lane] = at;
+    s_avail[wv][lane] = avail;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // 256 pieces of 16 bytes: piece p = lane + 64 i is slot p & 3 of block p >> 2
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t p = lane + 64u * (uint32_t)i, j = p >> 2, q = p & 3u;
+      const int64_t av = s_avail[wv][j] - 16 * (int64_t)q;
+      if (av <= 0) continue;
+      const uint32_t slot = (q + (j >> 1)) & 3u;
+      const uint4 k = *reinterpret_cast<const uint4*>(ks + j * 16 + 4 * slot);
+      const uint64_t a = s_at[wv][j] + 16 * q;
+      if (av >= 16) {
+        uint4 v;
+        __builtin_memcpy(&v, data + a, 16);
+        v.x ^= k.x;
+        v.y ^= k.y;
+        v.z ^= k.z;
+        v.w ^= k.w;
+        __builtin_memcpy(out + a, &v, 16);
+      } else {  // the chunk's last bytes: only its own (the next chunk's follow)
+        const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+        for (int64_t t = 0; t < av; t++)
+          out[a + t] = data[a + t] ^ (uint8_t)(kw[t >> 2] >> (8 * (t & 3)));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the window's keystream is read before the next one lands
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
 #undef PFS_CQR
 
 // 5c. BLAKE2b-256, one lane per segment.  No cross-lane traffic at all: the 16-word state,
@@ -2338,8 +2445,14 @@ hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pf
   // context's launches)
   const uint64_t need = (nblocks + 255) / 256,
                  full = (uint64_t)num_cus * (one_wave_per_simd ? 1 : 32);
-  chacha_xor_kernel<<<(unsigned)(need < full ? need : full), 256, 0, st>>>(
-      data, offs, segs, blk_base, n, refs, out, prio ? 1u : 0u);
+  const unsigned grid = (unsigned)(need < full ? need : full);
+  const char* e = getenv("PFSCDC_CHACHA_COALESCED");  // read per launch (tests switch it)
+  if (!(e && *e && atoi(e) == 0))
+    chacha_xor_coalesced_kernel<<<grid, kChachaBlock, 0, st>>>(data, offs, segs, blk_base, n,
+                                                              refs, out, prio ? 1u : 0u);
+  else
+    chacha_xor_kernel<<<grid, 256, 0, st>>>(data, offs, segs, blk_base, n, refs, out,
+                                            prio ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -217,8 +217,9 @@ def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkey
         assert bytes(refs0[i]["id"]) == rid and bytes(refs0[i]["dek"]) == dek
 
 
+@pytest.mark.parametrize("chacha_coalesced", ["1", "0"])
 @pytest.mark.parametrize("refid_split", ["0", "1"])
-def test_ciphertext_in_place_whatever_the_refid_form(refid_split, monkeypatch):
+def test_ciphertext_in_place_whatever_the_refid_form(refid_split, chacha_coalesced, monkeypatch):
     """In place, chunk.Create always takes the split Ref.Id form: the fused kernel's plaintext
     and ciphertext pointers are __restrict__ and must not alias, so PFSCDC_REFID_SPLIT=0 (or a
     chunk count above the quads, which picks the fused form) must not reach it with
@@ -233,6 +234,7 @@ def test_ciphertext_in_place_whatever_the_refid_form(refid_split, monkeypatch):
     streams = [0, len(lens) // 2, len(lens)]
     cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
     monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "0")
+    monkeypatch.setenv("PFSCDC_CHACHA_COALESCED", chacha_coalesced)
 
     def run(in_place, split_env):
         if split_env is None:
