@@ -1817,9 +1817,9 @@ PFS_DEV uint32_t rotl32v(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x
     x[c] += x[d]; x[b] = rotl32v(x[b] ^ x[c], 7);   \
   } while (0)
 __global__ __launch_bounds__(256) void chacha_xor_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    const uint8_t* data, const uint64_t* __restrict__ offs,
     const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
-    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio) {
+    const pfscdc_ref* __restrict__ refs, uint8_t* out, uint32_t prio) {
   if (prio) __builtin_amdgcn_s_setprio(2);  // the long chunk set's pass issues first
   const uint64_t nblocks = blk_base[n];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1892,11 +1892,13 @@ __global__ __launch_bounds__(256) void chacha_xor_kernel(
 // byte by byte up to the chunk's end (in place, the next chunk's first block is another
 // lane's).  c4 commit data plane at G = 2, same box, alternating: 369.5-369.9 -> 378.3-378.8
 // GiB/s (profiles/r4/chacha/).  PFSCDC_CHACHA_COALESCED=0: the per-lane form (A/B).
+// data and out are not __restrict__ in either ChaCha20 kernel: in place (PFSCDC_OPT_CTEXT_IN_PLACE)
+// they are the same buffer; every byte is read before the same lane writes it.
 constexpr int kChachaBlock = 256;
 __global__ __launch_bounds__(kChachaBlock) void chacha_xor_coalesced_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
+    const uint8_t* data, const uint64_t* __restrict__ offs,
     const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
-    const pfscdc_ref* __restrict__ refs, uint8_t* __restrict__ out, uint32_t prio) {
+    const pfscdc_ref* __restrict__ refs, uint8_t* out, uint32_t prio) {
   if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ __attribute__((aligned(16))) uint32_t s_ks[kChachaBlock / 64][64 * 16];
   __shared__ uint64_t s_at[kChachaBlock / 64][64];
