@@ -177,6 +177,19 @@ bool hash_fair_forced() {
   return on;
 }
 
+// Scan workgroups: one per CU (each takes a whole CU's LDS), at most the tiles.  A workgroup
+// that finds no CU free waits for one, and the launch ends only after every workgroup has run:
+// with other streams' chain-bound hash launches resident on some CUs (c3's streams in flight,
+// which reserve their CUs), a full-width scan waits for them.  PFSCDC_SCAN_GRID=n caps the
+// workgroups (read per launch; the work queue spreads the units over however many run).
+static int scan_grid(uint64_t ntiles, int num_cus) {
+  uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)num_cus);
+  const char* e = getenv("PFSCDC_SCAN_GRID");
+  const int cap = e ? atoi(e) : 0;
+  if (cap > 0 && (uint64_t)cap < g) g = (uint64_t)cap;
+  return (int)g;
+}
+
 // PFSCDC_HASH_CU_EXCLUSIVE=0: chain-bound scan hashes may share CUs with another launch (A/B)
 bool hash_cu_exclusive() {
   static const bool on = [] {
@@ -514,7 +527,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                                  c->d_skip.p, c->d_counts.p + 3, st));
       skip = c->d_skip.p;
     }
-    const int grid = (int)std::min<uint64_t>(c->ntiles, (uint64_t)c->num_cus);  // 1 WG per CU (LDS)
+    const int grid = scan_grid(c->ntiles, c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
                           c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1,
                           c->d_entries.p, c->d_counts.p, c->d_span.p, st, skip));
@@ -1305,7 +1318,7 @@ int pfscdc_candidates(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));
   HIP_OK(c, reset_spans(c, st));
   HIP_OK(c, hipEventRecord(c->ev[0], st));
-  const int grid = (int)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus);
+  const int grid = scan_grid(ntiles, c->num_cus);
   HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, c->params.average_bits, ntiles,
                         c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1, c->d_entries.p,
                         c->d_counts.p, c->d_span.p, st));
