@@ -331,27 +331,41 @@ def launch_ranks(gpus: int, argv) -> int:
     return subprocess.call(cmd, env=dict(os.environ))
 
 
-def hw_queues_setting() -> int:
+def hw_queues_setting(at_least: int = 8) -> int:
     """HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
-    share a queue and run one after the other: c3's four streams in flight (one context
-    each) and the commit's two chunk sets need a queue per stream.  Raised
-    to 8 (the box exports 4) before the first HIP call; a larger setting is kept.  The
-    effective value goes into the line's config."""
+    share a queue and run one after the other: c3's streams in flight (one context each) and
+    the commit's two chunk sets need a queue per stream.  Raised to
+    ``at_least`` (8; 32 for c3's twelve streams) before the first HIP call; a larger setting
+    is kept.  The effective value goes into the line's config."""
     try:
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
     except ValueError:
         q = 0
-    if q < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
-        q = 8
+    if q < at_least:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(at_least)
+        q = at_least
     return q
+
+
+C3_INFLIGHT, C3_QUEUES, C3_SCAN_GRID = 12, 32, 64
+
+
+def c3_streams(args) -> bool:
+    """configs[2] on one GPU: several 10 GiB streams in flight, one context each."""
+    return args.config == "c3" and args.path == "put" and args.gpus <= 1
 
 
 def main():
     args = parse()
     if needs_launch(args.gpus, os.environ):
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    hwq = hw_queues_setting()
+    c3s = c3_streams(args)
+    hwq = hw_queues_setting(C3_QUEUES if c3s else 8)
+    if c3s:
+        # a step's scan takes one workgroup per CU; with up to twelve chain-bound hash launches
+        # of the other streams holding CUs, capped workgroups never wait for them (the library
+        # reads PFSCDC_SCAN_GRID per launch; an explicit setting is kept)
+        os.environ.setdefault("PFSCDC_SCAN_GRID", str(C3_SCAN_GRID))
 
     import numpy as np
     import torch
@@ -403,13 +417,14 @@ def main():
     # One step at a time by default, so every kernel launch has the GPU to itself and its
     # duration (HIP events, in-kernel span and a kernel trace alike) is its own.  c3 (one
     # stream, bound by its longest 20 MB chains: ~175 ms per stream whatever else runs) runs
-    # four steps in flight on four contexts (one hardware queue each, GPU_MAX_HW_QUEUES);
+    # twelve steps in flight on twelve contexts with 32 hardware queues and scans capped at
+    # 64 workgroups (212 GiB/s at four on 8 queues -> 500-547, profiles/r4/c3_queues/);
     # c4/c5 two (the next commit's scan and hashes fill what the chain-bound hash leaves:
     # 824 -> 936 / 820 -> 883 GiB/s, profiles/r3/c4_inflight/);
     # c2's two-in-flight throughput is measured after the timed region (``two_in_flight``).
     # c4/c5 hold >= 16K chains per step through --group instead.
     S = args.inflight if args.inflight > 0 else (
-        4 if args.path == "put" and args.config == "c3" else
+        C3_INFLIGHT if args.path == "put" and args.config == "c3" else
         2 if args.path == "put" and args.config in ("c4", "c5") else 1)
     batches = []
     for k in range(S):
@@ -585,6 +600,8 @@ def main():
                                         "frac_at_clock": round(ach / pk, 4)})
 
     info = dict(work.info)
+    if c3s:
+        info["scan_grid"] = int(os.environ.get("PFSCDC_SCAN_GRID", "0") or 0)
     info.update({"steps_in_flight": S, "host_ahead": ahead,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},

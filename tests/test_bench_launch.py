@@ -74,3 +74,20 @@ def test_hw_queues_recorded(monkeypatch):
     assert bench.hw_queues_setting() == 8 and os.environ["GPU_MAX_HW_QUEUES"] == "8"
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
     assert bench.hw_queues_setting() == 16
+
+
+def test_c3_streams_get_queues():
+    # configs[2] on one GPU runs twelve streams in flight: 32 hardware queues before any HIP
+    # call (streams beyond the queues serialize), never lowered below an explicit setting
+    import types
+    a = types.SimpleNamespace(config="c3", path="put", gpus=1)
+    assert bench.c3_streams(a)
+    assert not bench.c3_streams(types.SimpleNamespace(config="c3", path="put", gpus=8))
+    assert not bench.c3_streams(types.SimpleNamespace(config="c2", path="put", gpus=1))
+    assert bench.C3_QUEUES <= 32  # the GPU pool refuses more
+
+
+def test_c3_queue_setting(monkeypatch):
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert bench.hw_queues_setting(bench.C3_QUEUES) == 32
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "32"
