@@ -116,7 +116,7 @@ def _files_rank_root(rank, world):
     return got.tobytes(), st, (b, e)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_gather_index_to_root_moves_live_records_only(world):
     from pfs_amd import _lib
 
