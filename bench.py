@@ -348,6 +348,7 @@ def hw_queues_setting(at_least: int = 8) -> int:
 
 
 C3_INFLIGHT, C3_QUEUES, C3_SCAN_GRID = 12, 32, 64
+LITERAL_INFLIGHT = 12  # configs1_literal: batches in flight (c2 lines take C3_QUEUES queues)
 
 
 def c3_streams(args) -> bool:
@@ -360,7 +361,7 @@ def main():
     if needs_launch(args.gpus, os.environ):
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     c3s = c3_streams(args)
-    hwq = hw_queues_setting(C3_QUEUES if c3s else 8)
+    hwq = hw_queues_setting(C3_QUEUES if c3s or args.config == "c2" else 8)
     if c3s:
         # a step's scan takes one workgroup per CU; with up to twelve chain-bound hash launches
         # of the other streams holding CUs, capped workgroups never wait for them (the library
@@ -858,10 +859,37 @@ def literal_batch(args, work, chunker, data, params, local, Chunker, torch):
             pair[(reps * 2 + k) % 2].wait()
     piped = (time.perf_counter() - t0) / (reps * 2)
     other.close()
+    # many batches in flight: LITERAL_INFLIGHT contexts (one stream and hardware queue each),
+    # every call still one configs[1] batch; the batches' ~4 MiB chains overlap instead of
+    # aggregating into one launch
+    k = LITERAL_INFLIGHT
+    many = [chunker] + [Chunker(params, device=local) for _ in range(k - 1)]
+    for c in many[1:]:
+        c.scan(view, offs)
+    torch.cuda.synchronize()
+    busy = [False] * k
+    nmany = 4 * k
+    t0 = time.perf_counter()
+    for i in range(nmany):
+        j = i % k
+        if busy[j]:
+            many[j].wait()
+        many[j].scan_async(view, offs)
+        busy[j] = True
+    for j in range(k):
+        if busy[j]:
+            many[j].wait()
+    piped_k = (time.perf_counter() - t0) / nmany
+    for c in many[1:]:
+        c.close()
     return {"value": round(sb / serial / GIB, 3), "unit": "GiB/s",
             "ms_per_batch": round(serial * 1e3, 3),
             "hash_span_ms_median": round(statistics.median(hs), 3),
             "two_in_flight_value": round(sb / piped / GIB, 3),
+            "many_in_flight": {"batches_in_flight": k, "value": round(sb / piped_k / GIB, 3),
+                               "ms_per_batch": round(piped_k * 1e3, 3),
+                               "note": "%d contexts on %d streams, one configs[1] batch per "
+                                       "call, %d batches" % (k, k, nmany)},
             "note": "one configs[1] batch (1024 x 4 MiB) per step, device-resident, no "
                     "aggregation: bound by the ~4 MiB serial BLAKE2b chains (DESIGN.md §4)"}
 
