@@ -1,4 +1,4 @@
-"""Multi-rank logic on CPU (gloo, world_size 2 and 3): every sharded form of the path
+"""Multi-rank logic on CPU (gloo, world_size 2, 3 and 4): every sharded form of the path
 produces exactly the single-process result.  On the GPU box the same code runs over RCCL
 ("nccl" backend) from bench.py; here the per-rank compute is the CPU oracle standing in for
 the GPU (the sharding, the collectives and the border copies are what is under test).
