@@ -4,4 +4,5 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 bash tools/r4_ab_env.sh r4ab_w8 "PFSCDC_LIB=pfs_amd/libpfscdc.so" "PFSCDC_LIB=pfs_amd/ab/libpfscdc_w8.so" 2 &&
-bash tools/r4_ab_env.sh r4ab_w4 "PFSCDC_LIB=pfs_amd/libpfscdc.so" "PFSCDC_LIB=pfs_amd/ab/libpfscdc_w4.so" 1
+bash tools/r4_ab_env.sh r4ab_w4 "PFSCDC_LIB=pfs_amd/libpfscdc.so" "PFSCDC_LIB=pfs_amd/ab/libpfscdc_w4.so" 1 &&
+bash tools/r4_ab_env.sh r4ab_w8a14 "PFSCDC_LIB=pfs_amd/libpfscdc.so" "PFSCDC_LIB=pfs_amd/ab/libpfscdc_w8a14.so" 1
