@@ -152,6 +152,10 @@ PFS_DEV const uint8_t* block_src(const uint8_t* data, const uint8_t* tail, uint6
 // Rare path: a block had a candidate; re-roll it byte by byte from its entry state and
 // record exact in-tile offsets (writer.go:167 test, positions >= 63 and < n only).  Bytes
 // are re-read from memory so the hot loop's register blocks are never indexed dynamically.
+// The unit's lowest candidate also goes to its slot of the tile record (the cut-skipping
+// scan reports it to the unit's file, scan_unit_report); the atomic is waited for here, so
+// the wave's own read-back at the end of the unit sees it.  Nothing beyond the tile record
+// is live across the hot loop for this.
 PFS_DEV void record_block(const uint8_t* __restrict__ data,
                                           const uint8_t* __restrict__ tail, uint64_t n_main,
                                           uint64_t h, uint64_t pos, uint64_t n,
@@ -160,6 +164,7 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
                                           TileRec* __restrict__ rec) {
   const uint8_t* in = block_src(data, tail, n_main, pos);
   const uint8_t* out = pos >= 64 ? block_src(data, tail, n_main, pos - 64) : nullptr;
+  uint32_t* const umin = &rec->umin[(pos - tile_base) / kScanUnit];
   for (int t = 0; t < 64; t++) {
     const uint64_t i = pos + t;
     const uint32_t bi = in[t];
@@ -169,6 +174,9 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
       // unordered; compact_kernel sorts the tile's offsets (count > kTileK marks it dense)
       const uint32_t k = atomicAdd(&rec->count, 1u);
       if (k < (uint32_t)kTileK) rec->off[k] = (uint32_t)(i - tile_base);
+      const uint32_t old = __hip_atomic_fetch_max(umin, ~(uint32_t)(i - tile_base),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::"v"(old));  // performed before this wave goes on
     }
   }
 }
@@ -430,13 +438,91 @@ PFS_DEV void span_end(uint64_t* span, SpanClock c) {
   }
 }
 
+// Cut skipping (ScanPlan), at the start of a unit: the unit behind dispatch slot `slot`
+// belongs to file f, `rank` units past the unit holding the file's first eligible position
+// E = fs + min - 1.  If the file's first cut is settled -- every unit up to the cut's own has
+// reported; the lowest candidate, else the forced cut at fs + max - 1 -- the positions after
+// it up to cut + min - 1 cannot be cuts either (writer.go:167-170 counts from the reset at the
+// cut, :211), and the unit skips its strip steps below cut + min.  The state word is read
+// with one returning agent-scope atomic; any value it returns is safe (its candidate half
+// already holds the candidates of every unit its done half names), a stale one just skips
+// less.
+PFS_DEV void scan_unit_plan(const ScanPlan* __restrict__ plan, uint64_t slot, uint32_t lane,
+                            uint64_t n, uint64_t& unit, uint32_t& skip, uint32_t& fr) {
+  const uint4 sl = plan->slots[slot];
+  unit = sl.x;
+  const uint32_t f = sl.y, rank = sl.z >> 8;
+  skip = sl.z & 0xffu;
+  const uint32_t mode = plan->mode;
+  fr = mode == 3 ? ~0u : f | (rank < 255 ? rank : 255u) << 24;
+  if (rank == 0 || mode != 1) return;  // nothing of the file before this unit (or A/B forms)
+  uint64_t st = 0;
+  if (lane == 0)
+    st = __hip_atomic_fetch_or(plan->fstate + f, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t e = plan->offs[f] + plan->min_chunk - 1;
+  const uint32_t inv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)st);
+  const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(st >> 32));
+  uint64_t cut_rel = plan->max_chunk - plan->min_chunk;  // forced: fs + max - 1 = E + this
+  if (inv && (uint64_t)(~inv) < cut_rel) cut_rel = ~inv;
+  const uint64_t cut = e + cut_rel;
+  const uint64_t j = cut / kScanUnit - e / kScanUnit;    // the rank of the cut's unit
+  const uint32_t need = (2u << (j < 31 ? j : 31)) - 1u;  // ranks 0..j reported
+  if (j >= rank || j >= 32 || (done & need) != need) return;
+  const uint64_t d = cut + plan->min_chunk;  // the next eligible position
+  const uint64_t ub = unit * kScanUnit;
+  if (d <= ub) return;
+  const uint64_t s2 = (d - ub) / kUnitStep;
+  const uint32_t ns = s2 < kUnitSteps ? (uint32_t)s2 : kUnitSteps;
+  if (ns <= skip) return;
+  if (lane == 0) {
+    const uint64_t ue = ub + kScanUnit < n ? ub + kScanUnit : n;
+    const uint64_t a = ub + skip * kUnitStep, b = ub + ns * kUnitStep;
+    atomicAdd(plan->dyn_skipped, (unsigned long long)((b < ue ? b : ue) - a));
+  }
+  skip = ns;
+}
+
+// Cut skipping, at the end of a unit of rank < 32: its lowest candidate (its slot of the tile
+// record, read back with a returning atomic: record_block waited for every update) goes to
+// the file's candidate half if it lies in [E, fe), then the unit's done bit; both are
+// agent-scope atomics on the file's word, the second issued after the first returned.  A
+// lowest candidate below E (the first strip step of the file's first unit can start up to
+// 8 KiB before E) hides whether one follows at or past E: that unit never reports done, and
+// the file's later units just roll everything.
+PFS_DEV void scan_unit_report(const ScanPlan* __restrict__ plan, uint32_t fr,
+                              TileRec* __restrict__ rec, uint64_t wslot, uint64_t tile_base,
+                              uint32_t lane) {
+  const uint32_t f = fr & (kPlanMaxFiles - 1), rank = fr >> 24;
+  if (rank >= 32) return;  // never waited for (a settled cut needs ranks 0..j, j < 32)
+  uint32_t w = 0;
+  if (lane == 0)
+    w = __hip_atomic_fetch_or(&rec->umin[wslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t e = plan->offs[f] + plan->min_chunk - 1, fe = plan->offs[f + 1];
+  w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+  uint32_t* const word = reinterpret_cast<uint32_t*>(plan->fstate + f);
+  if (w) {
+    const uint64_t c = tile_base + ~w;
+    if (c < e) return;
+    if (c < fe && c - e < 0xffffffffull && lane == 0) {
+      const uint32_t old = __hip_atomic_fetch_max(word, ~(uint32_t)(c - e), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::"v"(old));  // performed before the done bit goes out
+    }
+  }
+  if (lane == 0) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_fetch_or(word + 1, 1u << rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <bool WIDE, bool PAIR>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
     TileRec* __restrict__ recs, uint32_t* __restrict__ unit_ctr, uint32_t* __restrict__ done_ctr,
     uint64_t* __restrict__ entries, uint64_t* __restrict__ n_entries,
-    const uint32_t* __restrict__ unit_skip, uint64_t* span) {
+    const uint32_t* __restrict__ unit_skip, uint64_t* span,
+    const ScanPlan* __restrict__ plan) {
   const SpanClock span_clk = span_begin(span);
   // Dynamic LDS only (base address 0): [0, 64 KiB) table copies, then the per-wave staging
   // images.  recs[] is zeroed before the launch; candidates are added to it directly.
@@ -475,25 +561,33 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   // Work unit = one wave's 64 strips of a tile.  Each wave takes the next unit from a
   // launch-wide counter (zeroed before the launch), so CUs that start late (another step's
   // hash still draining there) simply take fewer units instead of finishing last.
-  const uint64_t nunits = ntiles * (uint64_t)kScanWaves;
+  // With a plan (cut skipping, ScanPlan in device memory) the counter runs over its
+  // rank-ordered slots instead of the units.  The next slot is taken at the end of a unit,
+  // before that unit reports to its file, so the two round trips overlap.
+  const uint64_t nunits = plan ? (uint64_t)plan->plan[0] : ntiles * (uint64_t)kScanWaves;
+  uint32_t u0 = 0;
+  if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);
   for (;;) {
-    uint32_t u0 = 0;
-    if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);
-    const uint64_t unit = (uint32_t)__builtin_amdgcn_readfirstlane(u0);
-    if (unit >= nunits) break;
+    const uint64_t slot = (uint32_t)__builtin_amdgcn_readfirstlane(u0);
+    if (slot >= nunits) break;
+    uint64_t unit = slot;
+    uint32_t skip = 0;
+    uint32_t fr = ~0u;  // the file this unit reports to | its rank << 24 (~0u: none)
+    if (plan) scan_unit_plan(plan, slot, lane, n, unit, skip, fr);
     const uint64_t tile = unit / kScanWaves;
     const uint64_t wslot = unit % kScanWaves;
 #else
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t wslot = wave;
+    uint32_t skip = 0;
 #endif
     TileRec* const rec = recs + tile;
     const uint64_t tile_base = tile * kTile;
     // Leading 128-byte steps of this unit's strips that hold no eligible position (inside
     // the first min - 1 bytes of a file: scan_skip_kernel); the strips then shrink to cover
     // the rest of the unit.  kStrip / 128 = the whole unit is skipped.
-    const uint32_t skip =
-        unit_skip ? (uint32_t)__builtin_amdgcn_readfirstlane((int)unit_skip[tile * kScanWaves + wslot]) : 0u;
+    if (unit_skip && !plan)
+      skip = (uint32_t)__builtin_amdgcn_readfirstlane((int)unit_skip[tile * kScanWaves + wslot]);
     const uint32_t nsteps = kStrip / 128 - skip, strip = nsteps * 128u;
     const uint64_t wave_base = tile_base + wslot * 64 * kStrip + (uint64_t)skip * (64 * 128);
     if (nsteps && wave_base < n) {  // wave-uniform
@@ -592,6 +686,10 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
         }
       }
     }
+#if PFS_SCAN_DYN
+    if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);  // the next unit, in flight during the report
+    if (fr != ~0u) scan_unit_report(plan, fr, rec, wslot, tile_base, lane);
+#endif
   }
   // the last workgroup compacts the tile records into the sorted entry list (the table and
   // staging LDS are free once every wave of the workgroup is past its last unit)
@@ -615,16 +713,28 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
 // their full 64-byte window (the halo load in front of each strip), so every candidate at an
 // eligible position is found exactly as before.  *scanned += the bytes left to scan.
 // One thread per unit; a unit spanning more than 64 files is scanned whole.
+//
+// With uinfo/plan (the cut-skipping scan, ScanPlan; min - 1 >= one unit, so a unit's
+// eligible positions all belong to the file holding its first one): uinfo[2u] = that file
+// (~0u: the unit is not scanned), uinfo[2u + 1] = skip | rank << 8, rank = the unit's index
+// past the unit holding the file's first eligible position; plan[2 + min(rank, 63)] counts
+// the units of each rank, and the last workgroup turns the counts into each rank's first
+// dispatch slot (plan[0] = the slots used).
 __global__ __launch_bounds__(256) void scan_skip_kernel(
     const uint64_t* __restrict__ offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
-    uint64_t nunits, uint32_t* __restrict__ skip, unsigned long long* __restrict__ scanned) {
-  constexpr uint64_t U = 64ull * kStrip, kStep = 64ull * 128;
-  constexpr uint32_t kAll = kStrip / 128;
+    uint64_t nunits, uint32_t* __restrict__ skip, unsigned long long* __restrict__ scanned,
+    uint32_t* __restrict__ uinfo, uint32_t* __restrict__ plan) {
+  constexpr uint64_t U = kScanUnit, kStep = kUnitStep;
+  constexpr uint32_t kAll = kUnitSteps;
+  __shared__ uint32_t s_flag;
+  __shared__ uint32_t s_hist[kPlanBuckets];  // this block's units per rank (one global add each)
+  if (uinfo && threadIdx.x < kPlanBuckets) s_hist[threadIdx.x] = 0;
+  if (uinfo) __syncthreads();
   const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long live = 0;
   if (u < nunits) {
     const uint64_t ub = u * U, ue = ub + U < n ? ub + U : n;
-    uint32_t s = kAll;
+    uint32_t s = kAll, tf = ~0u, rank = 0;
     if (ub < n) {
       // the file holding ub: the last f < nfiles with offs[f] <= ub (offs[nfiles] = n > ub)
       uint32_t lo = 0, hi = nfiles;
@@ -644,6 +754,8 @@ __global__ __launch_bounds__(256) void scan_skip_kernel(
         if (ls < fe) {  // the file's first eligible position; later files start beyond it
           const uint64_t first = ls > ub ? ls : ub;
           s = first < ue ? (uint32_t)((first - ub) / kStep) : kAll;
+          tf = f;
+          rank = (uint32_t)(ub / U - ls / U);  // ls <= first < ue: ls's unit is at most u
           break;
         }
       }
@@ -651,11 +763,59 @@ __global__ __launch_bounds__(256) void scan_skip_kernel(
       if (s < kAll) live = ue - (ub + s * kStep);
     }
     skip[u] = s;
+    if (uinfo) {
+      const bool scanned_unit = s < kAll;
+      uinfo[2 * u] = scanned_unit ? tf : ~0u;
+      uinfo[2 * u + 1] = s | (rank < 255 ? rank : 255u) << 8;
+      if (scanned_unit) atomicAdd(&s_hist[rank < kPlanBuckets - 1 ? rank : kPlanBuckets - 1], 1u);
+    }
   }
   // one atomic per wave
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
   if ((threadIdx.x & 63) == 0 && live) atomicAdd(scanned, live);
+  if (!uinfo) return;
+  __syncthreads();
+  if (threadIdx.x < kPlanBuckets && s_hist[threadIdx.x])
+    atomicAdd(&plan[2 + threadIdx.x], s_hist[threadIdx.x]);
+  if (last_block_done(&plan[1], &s_flag) && threadIdx.x == 0) {
+    uint32_t run = 0;  // each rank's count -> its first slot
+    for (uint32_t b = 0; b < kPlanBuckets; b++) {
+      const uint32_t c = __hip_atomic_load(&plan[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      plan[2 + b] = run;
+      run += c;
+    }
+    plan[0] = run;
+  }
+}
+
+// The cut-skipping scan's dispatch slots: every scanned unit at the next slot of its rank, a
+// block's units of one rank together (one global add per block and rank, then LDS).
+// Thread 0 also stores the plan header the scan kernel reads (its arguments by value here: no
+// host copy into device memory, which from pageable memory would block the host).
+__global__ __launch_bounds__(256) void scan_slots_kernel(uint64_t nunits,
+                                                         const uint32_t* __restrict__ uinfo,
+                                                         uint32_t* __restrict__ plan,
+                                                         uint4* __restrict__ slots,
+                                                         ScanPlan hdr, ScanPlan* __restrict__ d_hdr) {
+  __shared__ uint32_t s_cnt[kPlanBuckets], s_base[kPlanBuckets];
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u == 0) *d_hdr = hdr;
+  if (threadIdx.x < kPlanBuckets) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t f = ~0u, sr = 0, b = 0, local = 0;
+  if (u < nunits) {
+    f = uinfo[2 * u];
+    sr = uinfo[2 * u + 1];
+    const uint32_t rank = sr >> 8;
+    b = rank < kPlanBuckets - 1 ? rank : kPlanBuckets - 1;
+    if (f != ~0u) local = atomicAdd(&s_cnt[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kPlanBuckets && s_cnt[threadIdx.x])
+    s_base[threadIdx.x] = atomicAdd(&plan[2 + threadIdx.x], s_cnt[threadIdx.x]);
+  __syncthreads();
+  if (f != ~0u) slots[s_base[b] + local] = make_uint4((uint32_t)u, f, sr, 0u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2272,28 +2432,45 @@ hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, u
   const uint64_t nunits = ntiles * kScanWaves;
   if (nunits == 0) return hipSuccess;
   scan_skip_kernel<<<(unsigned)((nunits + 255) / 256), 256, 0, st>>>(
-      offs, nfiles, n, min_chunk, nunits, skip, (unsigned long long*)scanned);
+      offs, nfiles, n, min_chunk, nunits, skip, (unsigned long long*)scanned, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_plan(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
+                            uint64_t ntiles, uint32_t* skip, uint64_t* scanned, uint32_t* uinfo,
+                            uint4* slots, uint32_t* plan, const ScanPlan& hdr, ScanPlan* d_hdr,
+                            hipStream_t st) {
+  const uint64_t nunits = ntiles * kScanWaves;
+  if (nunits == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((nunits + 255) / 256);
+  scan_skip_kernel<<<grid, 256, 0, st>>>(offs, nfiles, n, min_chunk, nunits, skip,
+                                         (unsigned long long*)scanned, uinfo, plan);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  scan_slots_kernel<<<grid, 256, 0, st>>>(nunits, uinfo, plan, slots, hdr, d_hdr);
   return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
-                       uint64_t* n_entries, uint64_t* span, hipStream_t st, const uint32_t* skip) {
+                       uint64_t* n_entries, uint64_t* span, hipStream_t st, const uint32_t* skip,
+                       const ScanPlan* d_plan) {
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
+  const ScanPlan* const pl = d_plan;
   if (average_bits <= 32 && scan_pair())
     cdc_scan_kernel<false, true><<<grid, kScanBlock, lds, st>>>(
         data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
-        entries, n_entries, skip, span);
+        entries, n_entries, skip, span, pl);
   else if (average_bits <= 32)
     cdc_scan_kernel<false, false><<<grid, kScanBlock, lds, st>>>(
         data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
-        entries, n_entries, skip, span);
+        entries, n_entries, skip, span, pl);
   else
     cdc_scan_kernel<true, false><<<grid, kScanBlock, lds, st>>>(
         data, tail, n, d_table, 64 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
-        entries, n_entries, skip, span);
+        entries, n_entries, skip, span, pl);
   return hipGetLastError();
 }
 

@@ -87,8 +87,15 @@ struct pfscdc_ctx {
   DevBuf<TileRec> d_recs;
   DevBuf<uint32_t> d_unit_ctr;  // the scan's work-unit counter
   DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
+  // the cut-skipping scan (ScanPlan): per unit {file, skip | rank}, the rank-ordered
+  // dispatch slots, the plan words, per file its state word
+  DevBuf<uint32_t> d_uinfo, d_plan;
+  DevBuf<uint4> d_uslots;
+  DevBuf<uint64_t> d_fstate;
+  DevBuf<ScanPlan> d_planhdr;  // the scan kernel's view of the plan (scan_slots_kernel stores it)
   DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
-  bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned)
+  bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned,
+                                // less d_counts[6] the settled cuts removed)
   uint64_t scanned_bytes = 0;   // bytes the last waited-for scan rolled (copied in pfscdc_wait)
   bool cuts_only = false;       // the last pfscdc_scan left the DataRef hashes to commit_refs
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
@@ -206,6 +213,19 @@ bool scan_skip_enabled() {
     return !(e && atoi(e) == 0);
   }();
   return on;
+}
+
+// The scan also skips the min - 1 positions after each file's first cut once it is settled
+// (ScanPlan).  Exact for min - 1 >= one work unit and max - min < 2^32 - 1 (pfscdc_internal.h);
+// PFSCDC_SCAN_CUTSKIP=0 turns it off, 2 / 3 keep the rank order with reports / without and
+// never skip (A/B only: same results either way); read per launch.  Returns the mode, 0 = off.
+uint32_t cut_skip_mode(const pfscdc_params& p) {
+  const char* e = getenv("PFSCDC_SCAN_CUTSKIP");
+  const int m = e && *e ? atoi(e) : 1;
+  if (m < 1 || m > 3) return 0;
+  const bool exact = (uint64_t)p.min_chunk >= kScanUnit + 1 && p.max_chunk > p.min_chunk &&
+                     (uint64_t)(p.max_chunk - p.min_chunk) < 0xffffffffull;
+  return exact ? (uint32_t)m : 0u;
 }
 
 int fail(pfscdc_ctx* c, int code, const std::string& msg) {
@@ -353,6 +373,11 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_unit_ctr.release();
   c->d_entries.release();
   c->d_skip.release();
+  c->d_uinfo.release();
+  c->d_plan.release();
+  c->d_uslots.release();
+  c->d_fstate.release();
+  c->d_planhdr.release();
   c->d_counts.release();
   c->d_offs.release();
   c->d_seg_base.release();
@@ -486,10 +511,12 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, c->d_recs.ensure(c->ntiles));
   HIP_OK(c, c->d_unit_ctr.ensure(3));
   HIP_OK(c, c->d_entries.ensure(c->ntiles * kTileK + 1));
-  HIP_OK(c, c->d_counts.ensure(6));  // [4]: the hash queue's length (select), [5] fair share
+  // [3] bytes scanned, [4] the hash queue's length (select), [5] fair share, [6] bytes the
+  // settled cuts took off [3]
+  HIP_OK(c, c->d_counts.ensure(7));
   HIP_OK(c, c->d_tail.ensure(kTailBytes));
   HIP_OK(c, c->d_span.ensure(kSpanSlots));
-  HIP_OK(c, c->h_span.ensure(kSpanSlots + 1));
+  HIP_OK(c, c->h_span.ensure(kSpanSlots + 4));
 
   const uint8_t* data;
   if (bytes_on_device) {
@@ -510,7 +537,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   if (nbytes > n_main)
     HIP_OK(c, hipMemcpyAsync(c->d_tail.p, data + n_main, nbytes - n_main,
                              hipMemcpyDeviceToDevice, st));
-  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 6 * sizeof(uint64_t), st));
+  HIP_OK(c, hipMemsetAsync(c->d_counts.p, 0, 7 * sizeof(uint64_t), st));
   // the scan adds candidates to the tile records with atomics
   if (c->ntiles) HIP_OK(c, hipMemsetAsync(c->d_recs.p, 0, sizeof(TileRec) * c->ntiles, st));
   HIP_OK(c, hipMemsetAsync(c->d_unit_ctr.p, 0, 3 * sizeof(uint32_t), st));  // + done counters
@@ -521,16 +548,37 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     // the first min - 1 bytes of every file hold no cut point: those strip steps are skipped
     const uint32_t* skip = nullptr;
     c->scan_skipped = scan_skip_enabled();
+    const ScanPlan* d_plan = nullptr;
+    const uint64_t nunits = c->ntiles * kScanWaves;
     if (c->scan_skipped) {
-      HIP_OK(c, c->d_skip.ensure(c->ntiles * kScanWaves));
-      HIP_OK(c, launch_scan_skip(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,
-                                 c->d_skip.p, c->d_counts.p + 3, st));
+      HIP_OK(c, c->d_skip.ensure(nunits));
+      const uint32_t cs_mode = nfiles < kPlanMaxFiles ? cut_skip_mode(p) : 0u;
+      if (cs_mode) {
+        // and past each file's first cut, once it is settled (ScanPlan)
+        HIP_OK(c, c->d_uinfo.ensure(2 * nunits));
+        HIP_OK(c, c->d_uslots.ensure(nunits));
+        HIP_OK(c, c->d_plan.ensure(kPlanWords));
+        HIP_OK(c, c->d_fstate.ensure(nfiles));
+        HIP_OK(c, hipMemsetAsync(c->d_plan.p, 0, kPlanWords * sizeof(uint32_t), st));
+        HIP_OK(c, hipMemsetAsync(c->d_fstate.p, 0, nfiles * sizeof(uint64_t), st));
+        HIP_OK(c, c->d_planhdr.ensure(1));
+        const ScanPlan hdr{c->d_uslots.p, c->d_plan.p, c->d_fstate.p, c->d_offs.p,
+                           (uint64_t)p.min_chunk, (uint64_t)p.max_chunk,
+                           (unsigned long long*)(c->d_counts.p + 6), cs_mode};
+        HIP_OK(c, launch_scan_plan(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,
+                                   c->d_skip.p, c->d_counts.p + 3, c->d_uinfo.p, c->d_uslots.p,
+                                   c->d_plan.p, hdr, c->d_planhdr.p, st));
+        d_plan = c->d_planhdr.p;
+      } else {
+        HIP_OK(c, launch_scan_skip(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,
+                                   c->d_skip.p, c->d_counts.p + 3, st));
+      }
       skip = c->d_skip.p;
     }
     const int grid = scan_grid(c->ntiles, c->num_cus);  // 1 WG per CU (LDS)
     HIP_OK(c, launch_scan(data, c->d_tail.p, nbytes, c->d_table, p.average_bits, c->ntiles,
                           c->d_recs.p, grid, c->d_unit_ctr.p, c->d_unit_ctr.p + 1,
-                          c->d_entries.p, c->d_counts.p, c->d_span.p, st, skip));
+                          c->d_entries.p, c->d_counts.p, c->d_span.p, st, skip, d_plan));
   }
   HIP_OK(c, hipEventRecord(c->ev[1], st));
   HIP_OK(c, hipEventRecord(c->ev[2], st));
@@ -616,12 +664,12 @@ int pfscdc_wait(pfscdc_ctx* c) {
                            hipMemcpyDeviceToHost, c->stream));
   // the rolled-byte count now: later calls on this ctx reuse d_counts
   const bool skipped = c->scan_skipped && c->ntiles;
-  if (skipped)
-    HIP_OK(c, hipMemcpyAsync(c->h_span.p + kSpanSlots, c->d_counts.p + 3, sizeof(uint64_t),
+  if (skipped)  // [3] scanned after the first-min skip, [6] what the settled cuts took off
+    HIP_OK(c, hipMemcpyAsync(c->h_span.p + kSpanSlots, c->d_counts.p + 3, 4 * sizeof(uint64_t),
                              hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipEventRecord(c->ev[5], c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] : c->nbytes;
+  c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] - c->h_span.p[kSpanSlots + 3] : c->nbytes;
   c->nsegs = total;
   c->scan_valid = true;
   if (const char* wtrace = getenv("PFSCDC_WAVE_TRACE")) {  // development trace: append

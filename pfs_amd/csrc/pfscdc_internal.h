@@ -46,8 +46,13 @@ constexpr uint64_t kTailBytes = 256;  // zero-padded copy of the final partial 6
 struct TileRec {
   uint32_t count;
   uint32_t off[kTileK];
+  // per work unit (wave slot) of the tile: ~(its lowest candidate's offset in the tile), 0 =
+  // none; the cut-skipping scan reads its own unit's back when it reports to its file
+  uint32_t umin[kScanWaves];
+  uint32_t pad[16 - kScanWaves];
 };
-static_assert(sizeof(TileRec) == 64, "tile record is one 64-byte line");
+static_assert(kScanWaves <= 16, "unit minima fit the record's second line");
+static_assert(sizeof(TileRec) == 128, "tile record is two 64-byte lines");
 static_assert(sizeof(pfscdc_segment) == 56, "segment record layout");
 static_assert(sizeof(pfscdc_ref) == 64, "ref record layout");
 
@@ -100,15 +105,48 @@ uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
 hipError_t set_wave_trace(uint64_t* p, hipStream_t st);  // development trace (PFSCDC_WAVE_TRACE)
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
+
+// Scan work unit = one wave's 64 strips of a tile; kUnitSteps 128-byte strip steps of
+// kUnitStep bytes each.
+constexpr uint64_t kScanUnit = 64ull * kStrip;
+constexpr uint64_t kUnitStep = 64ull * 128;
+constexpr uint32_t kUnitSteps = kStrip / 128;
+// Cut skipping past a file's first cut (scan_skip_kernel + scan_slots_kernel): the work units go
+// out in rank order (the k-th unit past every file's first eligible position before any
+// file's (k+1)-th), each unit reports its candidates and its completion into its file's
+// state word, and a unit whose file's first cut is already settled skips the min - 1
+// positions after it.  Needs min - 1 >= kScanUnit (a unit's eligible positions then belong
+// to one file) and max - min < 2^32 - 1 (candidate offsets from the first eligible position
+// fit the state word).
+constexpr uint32_t kPlanBuckets = 64;  // ranks >= 63 share the last bucket
+constexpr uint32_t kPlanWords = 2 + kPlanBuckets;  // [0] slots used, [1] done ctr, cursors
+constexpr uint32_t kPlanMaxFiles = 1u << 24;       // a slot's file | rank << 24 in one word
+// in device memory (the scan kernel takes its address: one pointer live across the scan)
+struct ScanPlan {
+  const uint4* slots;     // per dispatch slot {unit, file, skip | rank << 8, 0}
+  const uint32_t* plan;   // plan words ([0] = slots used)
+  uint64_t* fstate;       // per file: lo = ~(first candidate - first eligible), hi = done ranks
+  const uint64_t* offs;   // file offsets (nfiles + 1)
+  uint64_t min_chunk, max_chunk;
+  unsigned long long* dyn_skipped;  // bytes the settled cuts removed from the scan
+  uint32_t mode;  // 1: skip past settled cuts; A/B only: 2 rank order + reports, 3 rank order
+};
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
                        uint32_t* unit_ctr, uint32_t* done_ctr, uint64_t* entries,
                        uint64_t* n_entries, uint64_t* span, hipStream_t st,
-                       const uint32_t* skip = nullptr);
+                       const uint32_t* skip = nullptr, const ScanPlan* d_plan = nullptr);
 // per scan work unit, the leading 128-B strip steps below its first eligible cut position
 // (file start + min - 1); *scanned += the bytes the scan still covers
 hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
                             uint64_t ntiles, uint32_t* skip, uint64_t* scanned, hipStream_t st);
+// the same, plus the rank-ordered dispatch slots of the cut-skipping scan: uinfo (2 words
+// per unit), slots (one per unit), plan (kPlanWords, zeroed), fstate (nfiles, zeroed); hdr
+// is stored at d_hdr for the scan kernel
+hipError_t launch_scan_plan(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
+                            uint64_t ntiles, uint32_t* skip, uint64_t* scanned, uint32_t* uinfo,
+                            uint4* slots, uint32_t* plan, const ScanPlan& hdr, ScanPlan* d_hdr,
+                            hipStream_t st);
 hipError_t launch_compact(const TileRec* recs, uint64_t ntiles, uint64_t n, uint64_t* entries,
                           uint64_t* n_entries, hipStream_t st);
 hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uint64_t* entries,
