@@ -778,14 +778,19 @@ __global__ __launch_bounds__(256) void scan_skip_kernel(
   __syncthreads();
   if (threadIdx.x < kPlanBuckets && s_hist[threadIdx.x])
     atomicAdd(&plan[2 + threadIdx.x], s_hist[threadIdx.x]);
-  if (last_block_done(&plan[1], &s_flag) && threadIdx.x == 0) {
-    uint32_t run = 0;  // each rank's count -> its first slot
-    for (uint32_t b = 0; b < kPlanBuckets; b++) {
-      const uint32_t c = __hip_atomic_load(&plan[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      plan[2 + b] = run;
-      run += c;
+  static_assert(kPlanBuckets == 64, "one wave turns the rank counts into first slots");
+  if (last_block_done(&plan[1], &s_flag) && threadIdx.x < 64) {
+    // each rank's count -> its first slot (a wave-wide exclusive scan)
+    const uint32_t c = __hip_atomic_load(&plan[2 + threadIdx.x], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if ((int)threadIdx.x >= o) x += y;
     }
-    plan[0] = run;
+    plan[2 + threadIdx.x] = x - c;
+    if (threadIdx.x == 63) plan[0] = x;
   }
 }
 
