@@ -219,15 +219,19 @@ int pfscdc_hash_ranges(pfscdc_ctx* ctx, const void* bytes, uint64_t nbytes, int 
                        const uint64_t* begins, const uint64_t* sizes, uint32_t n, uint8_t* out);
 
 /* Candidate positions (h & mask == 0, absolute offset >= 63) found by the last scan, sorted;
- * positions inside dense tiles are reported through the tile marker instead.  Debug/test
- * hook for the candidate-scan kernel. */
+ * positions inside dense tiles are reported through the tile marker instead.  Positions the
+ * scan skipped (see pfscdc_last_scan_bytes) are never listed.  Debug/test hook for the
+ * candidate-scan kernel. */
 uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
 
 /* Bytes the last pfscdc_scan's candidate kernel actually rolled.  Writer.roll never cuts in
  * the first min - 1 bytes after an Annotate (writer.go:125-128,167-170), so the scan skips
  * that part of every file (in 8 KiB steps of its work units) and the count is below nbytes
- * when files are longer than min; results are unchanged.  PFSCDC_SCAN_SKIP=0 (environment)
- * rolls every byte. */
+ * when files are longer than min; results are unchanged.  With min - 1 >= 256 KiB it also
+ * skips the min - 1 positions after a file's first cut once the scan has settled that cut
+ * (its work units go out in rank order and report per file), so the count then also depends
+ * on timing.  PFSCDC_SCAN_CUTSKIP=0 (environment, read per scan) keeps only the first skip;
+ * PFSCDC_SCAN_SKIP=0 rolls every byte. */
 int pfscdc_last_scan_bytes(pfscdc_ctx* ctx, uint64_t* out);
 
 /* Device timing of the last scan's kernels (ms, HIP events on the ctx stream):
