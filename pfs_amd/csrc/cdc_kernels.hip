@@ -152,19 +152,27 @@ PFS_DEV const uint8_t* block_src(const uint8_t* data, const uint8_t* tail, uint6
 // Rare path: a block had a candidate; re-roll it byte by byte from its entry state and
 // record exact in-tile offsets (writer.go:167 test, positions >= 63 and < n only).  Bytes
 // are re-read from memory so the hot loop's register blocks are never indexed dynamically.
-// The unit's lowest candidate also goes to its slot of the tile record (the cut-skipping
-// scan reports it to the unit's file, scan_unit_report); the atomic is waited for here, so
-// the wave's own read-back at the end of the unit sees it.  Nothing beyond the tile record
-// is live across the hot loop for this.
+// With a plan, the unit's lowest candidate also goes to its file's rank slot (an agent-scope
+// atomic max of kScanUnit - offset, waited for here, so the done bit the unit sets when it
+// ends can never be seen without it); the unit's file and rank come from the plan's per-unit
+// words, so nothing more is live across the hot loop for this than the plan pointer.
 PFS_DEV void record_block(const uint8_t* __restrict__ data,
                                           const uint8_t* __restrict__ tail, uint64_t n_main,
                                           uint64_t h, uint64_t pos, uint64_t n,
                                           uint64_t tile_base, uint64_t mask64,
                                           const uint64_t* __restrict__ table,
-                                          TileRec* __restrict__ rec) {
+                                          TileRec* __restrict__ rec,
+                                          const ScanPlan* __restrict__ plan) {
   const uint8_t* in = block_src(data, tail, n_main, pos);
   const uint8_t* out = pos >= 64 ? block_src(data, tail, n_main, pos - 64) : nullptr;
-  uint32_t* const umin = &rec->umin[(pos - tile_base) / kScanUnit];
+  uint32_t* rslot = nullptr;
+  uint64_t unit = pos;
+  asm volatile("" : "+v"(unit));  // computed here on the rare path, not hoisted into the hot one
+  unit /= kScanUnit;
+  if (plan) {
+    const uint32_t f = plan->uinfo[2 * unit], rank = plan->uinfo[2 * unit + 1] >> 8;
+    if (f != ~0u && rank < kRankSlots) rslot = plan->rslots + (uint64_t)f * kRankSlots + rank;
+  }
   for (int t = 0; t < 64; t++) {
     const uint64_t i = pos + t;
     const uint32_t bi = in[t];
@@ -174,9 +182,12 @@ PFS_DEV void record_block(const uint8_t* __restrict__ data,
       // unordered; compact_kernel sorts the tile's offsets (count > kTileK marks it dense)
       const uint32_t k = atomicAdd(&rec->count, 1u);
       if (k < (uint32_t)kTileK) rec->off[k] = (uint32_t)(i - tile_base);
-      const uint32_t old = __hip_atomic_fetch_max(umin, ~(uint32_t)(i - tile_base),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" ::"v"(old));  // performed before this wave goes on
+      if (rslot) {
+        const uint32_t old = __hip_atomic_fetch_max(
+            rslot, (uint32_t)(kScanUnit - (i - unit * kScanUnit)), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));  // performed before this wave goes on
+      }
     }
   }
 }
@@ -253,7 +264,7 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
     });                                                                                   \
     if (__builtin_expect(acc == 0, 0))                                                    \
       record_block(data, tail, n_main, ((uint64_t)hh0 << 32) | hl0, (POS), n, tile_base,  \
-                   mask64, table, rec);                                                   \
+                   mask64, table, rec, plan);                                             \
   }
 
 // --- narrow masks (average_bits <= 32): the rolling hash without the outgoing byte -----------
@@ -273,7 +284,7 @@ constexpr int kRollAhead = PFS_EXP_AHEAD;
 PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail,
                             uint64_t n_main, uint64_t pos, uint64_t n, uint64_t tile_base,
                             uint64_t mask64, const uint64_t* __restrict__ table,
-                            TileRec* __restrict__ rec) {
+                            TileRec* __restrict__ rec, const ScanPlan* __restrict__ plan) {
   uint64_t h = 0;
   if (pos >= 64) {
     const uint8_t* w = block_src(data, tail, n_main, pos - 64);
@@ -281,7 +292,7 @@ PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __r
   } else {
     for (int k = 0; k < 64; k++) h = rotl1_64(h) ^ table[0];
   }
-  record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, rec);
+  record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, rec, plan);
 }
 
 #ifndef PFS_SCAN_DYN
@@ -330,7 +341,7 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
       }                                                                                   \
     });                                                                                   \
     if (__builtin_expect(acc < cand_thr, 0))                                              \
-      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec);        \
+      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec, plan);  \
   }
 
 // --- the pair form of the g-recurrence (PAIR, narrow masks): two positions per 64-bit rotation --
@@ -398,7 +409,7 @@ PFS_DEV u32x4 lds_read_b128_async(uint32_t a) {
       }                                                                                   \
     });                                                                                   \
     if (__builtin_expect(acc < cand_thr, 0))                                              \
-      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec);        \
+      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec, plan);  \
   }
 
 // Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
@@ -438,15 +449,25 @@ PFS_DEV void span_end(uint64_t* span, SpanClock c) {
   }
 }
 
+PFS_DEV uint64_t readlane_u64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Cut skipping (ScanPlan), at the start of a unit: the unit behind dispatch slot `slot`
 // belongs to file f, `rank` units past the unit holding the file's first eligible position
-// E = fs + min - 1.  If the file's first cut is settled -- every unit up to the cut's own has
-// reported; the lowest candidate, else the forced cut at fs + max - 1 -- the positions after
-// it up to cut + min - 1 cannot be cuts either (writer.go:167-170 counts from the reset at the
-// cut, :211), and the unit skips its strip steps below cut + min.  The state word is read
-// with one returning agent-scope atomic; any value it returns is safe (its candidate half
-// already holds the candidates of every unit its done half names), a stale one just skips
-// less.
+// E = fs + min - 1.  One returning agent-scope atomic per lane reads the file's 64 rank slots
+// (a unit's slot holds its done bit and its lowest candidate, set in that order), then the
+// wave replays the selection (select_file, writer.go:163-189) over the ranks before this
+// one: from a segment's first eligible position lo, its cut is the first candidate at or past
+// lo within max - 1 bytes of the segment start, else the forced cut at start + max - 1;
+// settled when every rank from lo's up to the cut's has reported.  Each settled cut makes
+// the next min - 1 positions dead (the count restarts at the cut, writer.go:167-170, 211).
+// The unit skips its strip steps below the first eligible position after the last settled
+// cut.  The replay stops at the first unreported rank, at a rank past this unit's, or where a
+// rank's lowest candidate lies below lo in lo's own unit (another may follow in that unit);
+// every slot value is self-consistent, so a stale read only settles fewer cuts.
 PFS_DEV void scan_unit_plan(const ScanPlan* __restrict__ plan, uint64_t slot, uint32_t lane,
                             uint64_t n, uint64_t& unit, uint32_t& skip, uint32_t& fr) {
   const uint4 sl = plan->slots[slot];
@@ -456,19 +477,41 @@ PFS_DEV void scan_unit_plan(const ScanPlan* __restrict__ plan, uint64_t slot, ui
   const uint32_t mode = plan->mode;
   fr = mode == 3 ? ~0u : f | (rank < 255 ? rank : 255u) << 24;
   if (rank == 0 || mode != 1) return;  // nothing of the file before this unit (or A/B forms)
-  uint64_t st = 0;
-  if (lane == 0)
-    st = __hip_atomic_fetch_or(plan->fstate + f, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t e = plan->offs[f] + plan->min_chunk - 1;
-  const uint32_t inv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)st);
-  const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(st >> 32));
-  uint64_t cut_rel = plan->max_chunk - plan->min_chunk;  // forced: fs + max - 1 = E + this
-  if (inv && (uint64_t)(~inv) < cut_rel) cut_rel = ~inv;
-  const uint64_t cut = e + cut_rel;
-  const uint64_t j = cut / kScanUnit - e / kScanUnit;    // the rank of the cut's unit
-  const uint32_t need = (2u << (j < 31 ? j : 31)) - 1u;  // ranks 0..j reported
-  if (j >= rank || j >= 32 || (done & need) != need) return;
-  const uint64_t d = cut + plan->min_chunk;  // the next eligible position
+  const uint32_t v = __hip_atomic_fetch_or(plan->rslots + (uint64_t)f * kRankSlots + lane, 0u,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t fs = plan->offs[f], fe = plan->offs[f + 1];
+  const uint64_t mn = plan->min_chunk, mx = plan->max_chunk;
+  const uint64_t e = fs + mn - 1, u0 = e / kScanUnit;  // u0: the unit of rank 0
+  const uint64_t done_m = __ballot((v & kSlotDone) != 0);
+  const uint32_t inv = v & ~kSlotDone;  // kScanUnit - the lowest candidate's offset, 0: none
+  const uint64_t cand_m = __ballot(inv != 0);
+  const uint64_t cpos = (u0 + lane + 1) * kScanUnit - inv;  // lane q: rank q's lowest candidate
+  const uint64_t rlim = rank < kRankSlots ? rank : kRankSlots;
+  uint64_t lo = e, hi = fs + mx - 1, d = 0;
+  for (uint32_t it = 0; it < kRankSlots; it++) {
+    const uint64_t qlo = lo / kScanUnit - u0;  // the rank holding lo
+    if (qlo >= rlim) break;
+    const uint64_t from = cand_m & (~0ull << qlo);
+    const uint32_t qc = from ? (uint32_t)__builtin_ctzll(from) : 64u;
+    const uint64_t c = qc < 64 ? readlane_u64(cpos, qc) : ~0ull;
+    if (qc == qlo && c < lo) break;  // lo's own unit: a later candidate may follow its lowest
+    uint64_t cut, qneed;
+    if (c <= hi && c < fe) {
+      cut = c;
+      qneed = qc;
+    } else {
+      if (hi >= fe) break;  // the file ends first: no more cuts
+      cut = hi;             // forced (writer.go:179)
+      qneed = hi / kScanUnit - u0;
+    }
+    if (qneed >= rlim) break;
+    const uint64_t need = (qneed >= 63 ? ~0ull : (2ull << qneed) - 1) & (~0ull << qlo);
+    if ((done_m & need) != need) break;
+    d = cut + mn;  // the next eligible position
+    lo = d;
+    hi = cut + mx;
+  }
+  if (d == 0) return;
   const uint64_t ub = unit * kScanUnit;
   if (d <= ub) return;
   const uint64_t s2 = (d - ub) / kUnitStep;
@@ -482,37 +525,14 @@ PFS_DEV void scan_unit_plan(const ScanPlan* __restrict__ plan, uint64_t slot, ui
   skip = ns;
 }
 
-// Cut skipping, at the end of a unit of rank < 32: its lowest candidate (its slot of the tile
-// record, read back with a returning atomic: record_block waited for every update) goes to
-// the file's candidate half if it lies in [E, fe), then the unit's done bit; both are
-// agent-scope atomics on the file's word, the second issued after the first returned.  A
-// lowest candidate below E (the first strip step of the file's first unit can start up to
-// 8 KiB before E) hides whether one follows at or past E: that unit never reports done, and
-// the file's later units just roll everything.
-PFS_DEV void scan_unit_report(const ScanPlan* __restrict__ plan, uint32_t fr,
-                              TileRec* __restrict__ rec, uint64_t wslot, uint64_t tile_base,
-                              uint32_t lane) {
+// Cut skipping, at the end of a unit: its done bit into its rank slot (its lowest candidate
+// is there already: record_block waited for each update).  No reply is needed.
+PFS_DEV void scan_unit_report(const ScanPlan* __restrict__ plan, uint32_t fr, uint32_t lane) {
   const uint32_t f = fr & (kPlanMaxFiles - 1), rank = fr >> 24;
-  if (rank >= 32) return;  // never waited for (a settled cut needs ranks 0..j, j < 32)
-  uint32_t w = 0;
-  if (lane == 0)
-    w = __hip_atomic_fetch_or(&rec->umin[wslot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t e = plan->offs[f] + plan->min_chunk - 1, fe = plan->offs[f + 1];
-  w = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
-  uint32_t* const word = reinterpret_cast<uint32_t*>(plan->fstate + f);
-  if (w) {
-    const uint64_t c = tile_base + ~w;
-    if (c < e) return;
-    if (c < fe && c - e < 0xffffffffull && lane == 0) {
-      const uint32_t old = __hip_atomic_fetch_max(word, ~(uint32_t)(c - e), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" ::"v"(old));  // performed before the done bit goes out
-    }
-  }
-  if (lane == 0) {
-    asm volatile("" ::: "memory");
-    __hip_atomic_fetch_or(word + 1, 1u << rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (rank >= kRankSlots || lane != 0) return;
+  asm volatile("" ::: "memory");
+  __hip_atomic_fetch_or(plan->rslots + (uint64_t)f * kRankSlots + rank, kSlotDone,
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool WIDE, bool PAIR>
@@ -688,7 +708,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     }
 #if PFS_SCAN_DYN
     if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);  // the next unit, in flight during the report
-    if (fr != ~0u) scan_unit_report(plan, fr, rec, wslot, tile_base, lane);
+    if (fr != ~0u) scan_unit_report(plan, fr, lane);
 #endif
   }
   // the last workgroup compacts the tile records into the sorted entry list (the table and

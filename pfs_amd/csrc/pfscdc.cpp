@@ -88,10 +88,10 @@ struct pfscdc_ctx {
   DevBuf<uint32_t> d_unit_ctr;  // the scan's work-unit counter
   DevBuf<uint32_t> d_skip;      // per scan work unit: leading strip steps with no cut point
   // the cut-skipping scan (ScanPlan): per unit {file, skip | rank}, the rank-ordered
-  // dispatch slots, the plan words, per file its state word
+  // dispatch slots, the plan words, per file its rank slots
   DevBuf<uint32_t> d_uinfo, d_plan;
   DevBuf<uint4> d_uslots;
-  DevBuf<uint64_t> d_fstate;
+  DevBuf<uint32_t> d_rslots;
   DevBuf<ScanPlan> d_planhdr;  // the scan kernel's view of the plan (scan_slots_kernel stores it)
   DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned,
@@ -215,16 +215,15 @@ bool scan_skip_enabled() {
   return on;
 }
 
-// The scan also skips the min - 1 positions after each file's first cut once it is settled
-// (ScanPlan).  Exact for min - 1 >= one work unit and max - min < 2^32 - 1 (pfscdc_internal.h);
-// PFSCDC_SCAN_CUTSKIP=0 turns it off, 2 / 3 keep the rank order with reports / without and
-// never skip (A/B only: same results either way); read per launch.  Returns the mode, 0 = off.
+// The scan also skips the min - 1 positions after each file's cuts once they are settled
+// (ScanPlan).  Exact for min - 1 >= one work unit (pfscdc_internal.h).  PFSCDC_SCAN_CUTSKIP=0
+// turns it off, 2 / 3 keep the rank order with reports / without and never skip (A/B only:
+// same results either way); read per launch.  Returns the mode, 0 = off.
 uint32_t cut_skip_mode(const pfscdc_params& p) {
   const char* e = getenv("PFSCDC_SCAN_CUTSKIP");
   const int m = e && *e ? atoi(e) : 1;
   if (m < 1 || m > 3) return 0;
-  const bool exact = (uint64_t)p.min_chunk >= kScanUnit + 1 && p.max_chunk > p.min_chunk &&
-                     (uint64_t)(p.max_chunk - p.min_chunk) < 0xffffffffull;
+  const bool exact = (uint64_t)p.min_chunk >= kScanUnit + 1 && p.max_chunk > p.min_chunk;
   return exact ? (uint32_t)m : 0u;
 }
 
@@ -376,7 +375,7 @@ int pfscdc_ctx_destroy(pfscdc_ctx* c) {
   c->d_uinfo.release();
   c->d_plan.release();
   c->d_uslots.release();
-  c->d_fstate.release();
+  c->d_rslots.release();
   c->d_planhdr.release();
   c->d_counts.release();
   c->d_offs.release();
@@ -558,11 +557,11 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
         HIP_OK(c, c->d_uinfo.ensure(2 * nunits));
         HIP_OK(c, c->d_uslots.ensure(nunits));
         HIP_OK(c, c->d_plan.ensure(kPlanWords));
-        HIP_OK(c, c->d_fstate.ensure(nfiles));
+        HIP_OK(c, c->d_rslots.ensure((size_t)nfiles * kRankSlots));
         HIP_OK(c, hipMemsetAsync(c->d_plan.p, 0, kPlanWords * sizeof(uint32_t), st));
-        HIP_OK(c, hipMemsetAsync(c->d_fstate.p, 0, nfiles * sizeof(uint64_t), st));
+        HIP_OK(c, hipMemsetAsync(c->d_rslots.p, 0, (size_t)nfiles * kRankSlots * sizeof(uint32_t), st));
         HIP_OK(c, c->d_planhdr.ensure(1));
-        const ScanPlan hdr{c->d_uslots.p, c->d_plan.p, c->d_fstate.p, c->d_offs.p,
+        const ScanPlan hdr{c->d_uslots.p, c->d_plan.p, c->d_uinfo.p, c->d_rslots.p, c->d_offs.p,
                            (uint64_t)p.min_chunk, (uint64_t)p.max_chunk,
                            (unsigned long long*)(c->d_counts.p + 6), cs_mode};
         HIP_OK(c, launch_scan_plan(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,

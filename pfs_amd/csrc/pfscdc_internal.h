@@ -46,13 +46,8 @@ constexpr uint64_t kTailBytes = 256;  // zero-padded copy of the final partial 6
 struct TileRec {
   uint32_t count;
   uint32_t off[kTileK];
-  // per work unit (wave slot) of the tile: ~(its lowest candidate's offset in the tile), 0 =
-  // none; the cut-skipping scan reads its own unit's back when it reports to its file
-  uint32_t umin[kScanWaves];
-  uint32_t pad[16 - kScanWaves];
 };
-static_assert(kScanWaves <= 16, "unit minima fit the record's second line");
-static_assert(sizeof(TileRec) == 128, "tile record is two 64-byte lines");
+static_assert(sizeof(TileRec) == 64, "tile record is one 64-byte line");
 static_assert(sizeof(pfscdc_segment) == 56, "segment record layout");
 static_assert(sizeof(pfscdc_ref) == 64, "ref record layout");
 
@@ -111,21 +106,24 @@ hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSe
 constexpr uint64_t kScanUnit = 64ull * kStrip;
 constexpr uint64_t kUnitStep = 64ull * 128;
 constexpr uint32_t kUnitSteps = kStrip / 128;
-// Cut skipping past a file's first cut (scan_skip_kernel + scan_slots_kernel): the work units go
-// out in rank order (the k-th unit past every file's first eligible position before any
-// file's (k+1)-th), each unit reports its candidates and its completion into its file's
-// state word, and a unit whose file's first cut is already settled skips the min - 1
-// positions after it.  Needs min - 1 >= kScanUnit (a unit's eligible positions then belong
-// to one file) and max - min < 2^32 - 1 (candidate offsets from the first eligible position
-// fit the state word).
+// Cut skipping past settled cuts (scan_skip_kernel + scan_slots_kernel): the
+// work units go out in rank order (rank = the unit's index past the unit holding its file's
+// first eligible position; every file's rank-k unit before any file's rank-(k+1) unit); each
+// unit of rank < kRankSlots leaves one 32-bit word in its file's rank slots -- done bit, and
+// kScanUnit - (its lowest candidate's offset in the unit) -- and a unit that finds the file's
+// cuts before it settled by those slots skips the min - 1 positions after the last of them.
+// Needs min - 1 >= kScanUnit: a unit's eligible positions then belong to one file.
 constexpr uint32_t kPlanBuckets = 64;  // ranks >= 63 share the last bucket
 constexpr uint32_t kPlanWords = 2 + kPlanBuckets;  // [0] slots used, [1] done ctr, cursors
 constexpr uint32_t kPlanMaxFiles = 1u << 24;       // a slot's file | rank << 24 in one word
+constexpr uint32_t kRankSlots = 64;                // per file: one wave reads them all
+constexpr uint32_t kSlotDone = 1u << 31;
 // in device memory (the scan kernel takes its address: one pointer live across the scan)
 struct ScanPlan {
   const uint4* slots;     // per dispatch slot {unit, file, skip | rank << 8, 0}
   const uint32_t* plan;   // plan words ([0] = slots used)
-  uint64_t* fstate;       // per file: lo = ~(first candidate - first eligible), hi = done ranks
+  const uint32_t* uinfo;  // per unit {file (~0u: not scanned), skip | rank << 8}
+  uint32_t* rslots;       // per file kRankSlots words (zeroed before the scan)
   const uint64_t* offs;   // file offsets (nfiles + 1)
   uint64_t min_chunk, max_chunk;
   unsigned long long* dyn_skipped;  // bytes the settled cuts removed from the scan
@@ -141,7 +139,7 @@ hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, con
 hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
                             uint64_t ntiles, uint32_t* skip, uint64_t* scanned, hipStream_t st);
 // the same, plus the rank-ordered dispatch slots of the cut-skipping scan: uinfo (2 words
-// per unit), slots (one per unit), plan (kPlanWords, zeroed), fstate (nfiles, zeroed); hdr
+// per unit), slots (one per unit), plan (kPlanWords, zeroed); hdr
 // is stored at d_hdr for the scan kernel
 hipError_t launch_scan_plan(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
                             uint64_t ntiles, uint32_t* skip, uint64_t* scanned, uint32_t* uinfo,
