@@ -228,7 +228,7 @@ uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
  * the first min - 1 bytes after an Annotate (writer.go:125-128,167-170), so the scan skips
  * that part of every file (in 8 KiB steps of its work units) and the count is below nbytes
  * when files are longer than min; results are unchanged.  With min - 1 >= 256 KiB it also
- * skips the min - 1 positions after a file's first cut once the scan has settled that cut
+ * skips the min - 1 positions after every cut of a file that the scan has already settled
  * (its work units go out in rank order and report per file), so the count then also depends
  * on timing.  PFSCDC_SCAN_CUTSKIP=0 (environment, read per scan) keeps only the first skip;
  * PFSCDC_SCAN_SKIP=0 rolls every byte. */

@@ -553,7 +553,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
       HIP_OK(c, c->d_skip.ensure(nunits));
       const uint32_t cs_mode = nfiles < kPlanMaxFiles ? cut_skip_mode(p) : 0u;
       if (cs_mode) {
-        // and past each file's first cut, once it is settled (ScanPlan)
+        // and past every cut the scan has settled (ScanPlan: rank order, per-file rank slots)
         HIP_OK(c, c->d_uinfo.ensure(2 * nunits));
         HIP_OK(c, c->d_uslots.ensure(nunits));
         HIP_OK(c, c->d_plan.ensure(kPlanWords));
