@@ -551,7 +551,11 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     const uint64_t nunits = c->ntiles * kScanWaves;
     if (c->scan_skipped) {
       HIP_OK(c, c->d_skip.ensure(nunits));
-      const uint32_t cs_mode = nfiles < kPlanMaxFiles ? cut_skip_mode(p) : 0u;
+      // (the rank slots cost 256 B per file: batches of mostly tiny files, where it gains
+      // nothing, keep the plain form)
+      const bool cs_room = nfiles < kPlanMaxFiles &&
+                           (uint64_t)nfiles * kRankSlots * sizeof(uint32_t) * 64 <= nbytes;
+      const uint32_t cs_mode = cs_room ? cut_skip_mode(p) : 0u;
       if (cs_mode) {
         // and past every cut the scan has settled (ScanPlan: rank order, per-file rank slots)
         HIP_OK(c, c->d_uinfo.ensure(2 * nunits));
