@@ -607,6 +607,11 @@ def main():
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},
                  "gpu_max_hw_queues": ctx["hwq"],
+                 # the scan's skipping: first min - 1 bytes of each file, and past
+                 # every settled cut (1) unless PFSCDC_SCAN_CUTSKIP / PFSCDC_SCAN_SKIP say 0
+                 "scan_skip": {"first_min": os.environ.get("PFSCDC_SCAN_SKIP", "1") != "0",
+                               "cut_skip_mode": int(os.environ.get("PFSCDC_SCAN_CUTSKIP", "1")
+                                                    or 1)},
                  "parallelism": ("%s-sharded x%d, chunk-ref index gathered to rank 0 every "
                                  "step (%s: counts all-gathered, live records sent point to "
                                  "point)" % ("file" if args.config == "c2" else "fileset",
