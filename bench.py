@@ -364,8 +364,9 @@ def main():
     hwq = hw_queues_setting(C3_QUEUES if c3s or args.config == "c2" else 8)
     if c3s:
         # a step's scan takes one workgroup per CU; with up to twelve chain-bound hash launches
-        # of the other streams holding CUs, capped workgroups never wait for them (the library
-        # reads PFSCDC_SCAN_GRID per launch; an explicit setting is kept)
+        # of the other streams holding CUs, capped workgroups never wait for them (the
+        # PFSCDC_SCAN_GRID knob, read from the environment when the library first uses a knob;
+        # an explicit setting is kept)
         os.environ.setdefault("PFSCDC_SCAN_GRID", str(C3_SCAN_GRID))
 
     import numpy as np
@@ -600,18 +601,24 @@ def main():
                                         "peak_at_clock": round(pk, 1),
                                         "frac_at_clock": round(ach / pk, 4)})
 
+    from pfs_amd import _lib
+
     info = dict(work.info)
     if c3s:
-        info["scan_grid"] = int(os.environ.get("PFSCDC_SCAN_GRID", "0") or 0)
+        info["scan_grid"] = _lib.get_knob("PFSCDC_SCAN_GRID")
+    try:
+        smode = chunkers[0].last_scan_mode()
+    except Exception:  # noqa: BLE001 - a path without a batch scan
+        smode = 0
     info.update({"steps_in_flight": S, "host_ahead": ahead,
                  "params": {"average_bits": params.average_bits, "seed": params.seed,
                             "min": params.min_chunk, "max": params.max_chunk},
                  "gpu_max_hw_queues": ctx["hwq"],
-                 # the scan's skipping: first min - 1 bytes of each file, and past
-                 # every settled cut (1) unless PFSCDC_SCAN_CUTSKIP / PFSCDC_SCAN_SKIP say 0
-                 "scan_skip": {"first_min": os.environ.get("PFSCDC_SCAN_SKIP", "1") != "0",
-                               "cut_skip_mode": int(os.environ.get("PFSCDC_SCAN_CUTSKIP", "1")
-                                                    or 1)},
+                 # the scan's skipping as the library did it in the last step
+                 # (pfscdc_last_scan_mode): the first min - 1 bytes of each file, and past every
+                 # settled cut
+                 "scan_skip": {"first_min": bool(smode & _lib.SCAN_SKIPPED_FIRST_MIN),
+                               "past_settled_cuts": bool(smode & _lib.SCAN_SKIPPED_CUTS)},
                  "parallelism": ("%s-sharded x%d, chunk-ref index gathered to rank 0 every "
                                  "step (%s: counts all-gathered, live records sent point to "
                                  "point)" % ("file" if args.config == "c2" else "fileset",
@@ -1413,10 +1420,11 @@ def bench_uw(args, ctx):
     for i in range(p0, p1):
         o = int(pieces.offs[i - p0])
         views[(int(lay.file[i]), int(lay.start[i]))] = memoryview(host[o:o + int(lay.size[i])])
+    from pfs_amd import _lib
     if args.uw_workers > 0:
-        os.environ["PFSCDC_UW_WORKERS"] = str(args.uw_workers)
+        _lib.set_knob("PFSCDC_UW_WORKERS", args.uw_workers)
     if args.uw_group > 0:
-        os.environ["PFSCDC_UW_INFLIGHT"] = str(args.uw_group)
+        _lib.set_knob("PFSCDC_UW_INFLIGHT", args.uw_group)
     st = pf.Storage(ctx["local"], params, args.mem_threshold)
 
     def step():
@@ -1478,7 +1486,7 @@ def bench_uw(args, ctx):
         "stages_note": "per step; put_copy on the Put thread, the rest summed over the group "
                        "writes (a background thread per group writer, %s writer(s), each on its own ctx), "
                        "so they overlap the Puts and each other (pfscdc_uw_timings)"
-                       % os.environ.get("PFSCDC_UW_WORKERS", "1"),
+                       % _lib.get_knob("PFSCDC_UW_WORKERS"),
     }
     if stages.get("put_copy"):
         out["put_copy_gb_s"] = round(nbytes / (stages["put_copy"] * 1e-3) / 1e9, 2)

@@ -230,8 +230,8 @@ uint64_t pfscdc_debug_candidates(pfscdc_ctx* ctx, uint64_t* out, uint64_t cap);
  * when files are longer than min; results are unchanged.  With min - 1 >= 256 KiB it also
  * skips the min - 1 positions after every cut of a file that the scan has already settled
  * (its work units go out in rank order and report per file), so the count then also depends
- * on timing.  PFSCDC_SCAN_CUTSKIP=0 (environment, read per scan) keeps only the first skip;
- * PFSCDC_SCAN_SKIP=0 rolls every byte. */
+ * on timing.  The knob PFSCDC_SCAN_CUTSKIP=0 keeps only the first skip; PFSCDC_SCAN_SKIP=0
+ * rolls every byte (pfscdc_last_scan_mode tells which skipping the last scan did). */
 int pfscdc_last_scan_bytes(pfscdc_ctx* ctx, uint64_t* out);
 
 /* Device timing of the last scan's kernels (ms, HIP events on the ctx stream):
@@ -438,9 +438,13 @@ int pfscdc_uw_put(pfscdc_uwriter* w, const char* path, const char* tag, int appe
  * and the live files of the filesets this writer serialized; no parent fileset). */
 int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag);
 int pfscdc_uw_close(pfscdc_uwriter* w); /* serializes the rest (Close, :171-179) */
-/* Serialized filesets are written in groups of up to PFSCDC_UW_INFLIGHT bytes (env, default
+/* Serialized filesets are written in groups of up to PFSCDC_UW_INFLIGHT bytes (knob, default
  * 32 GiB) on a background thread while Puts continue; the event callback may run on that
- * thread (one group at a time, events in order).  Filesets are readable after Close. */
+ * thread, never on two threads at once.  Order: within one (fileset, index, level) stream,
+ * and within each fileset's data stream, events come in stream order; a group's data-stream
+ * events come fileset by fileset, but its index streams are closed level by level across the
+ * group's filesets, so index events of different filesets (and additive and deletive ones)
+ * interleave.  Filesets are readable after Close. */
 uint32_t pfscdc_uw_num_filesets(const pfscdc_uwriter* w);
 /* Fileset i's Primitive (pointers valid until pfscdc_uw_destroy). */
 int pfscdc_uw_fileset(const pfscdc_uwriter* w, uint32_t i, pfscdc_fileset_info* out);
@@ -473,6 +477,28 @@ uint64_t pfscdc_uw_cached_arena_bytes(void);
 
 /* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
 int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);
+
+/* ---- tuning knobs (no reference counterpart; INTEGRATION.md lists each with its range) ----
+ * Every knob is one process-wide integer named after its environment variable (PFSCDC_*).
+ * The library reads the environment once, the first time any knob is used; an unset, empty,
+ * non-numeric or out-of-range variable leaves the default (a bad value is reported on stderr).
+ * No knob changes any result: they select between exact forms of the same computation or size
+ * the host-fed writer's pools.  pfscdc_set_knob changes a knob for the whole process (atomic:
+ * a launch already enqueued keeps the value it read; the host-fed writer reads its knobs when
+ * it is created).  PFSCDC_EINVAL for an unknown name or a value outside the knob's range. */
+int pfscdc_set_knob(const char* name, int64_t value);
+int pfscdc_get_knob(const char* name, int64_t* value);
+/* The i-th knob's name (0-based), NULL past the last; lo/hi (nullable) its range and def
+ * (nullable) its built-in default. */
+const char* pfscdc_knob_info(int i, int64_t* lo, int64_t* hi, int64_t* def);
+
+/* How the last pfscdc_scan on ctx skipped bytes (bit set): PFSCDC_SCAN_SKIPPED_FIRST_MIN =
+ * the first min - 1 bytes of each file were not rolled; PFSCDC_SCAN_SKIPPED_CUTS = the scan
+ * also skipped past the cuts it had settled (rank-ordered units; needs min - 1 >= 256 KiB and
+ * at most one file per 16 KiB of the batch).  0: every byte was rolled. */
+#define PFSCDC_SCAN_SKIPPED_FIRST_MIN 1u
+#define PFSCDC_SCAN_SKIPPED_CUTS 2u
+int pfscdc_last_scan_mode(pfscdc_ctx* ctx, uint32_t* mode);
 
 #ifdef __cplusplus
 }

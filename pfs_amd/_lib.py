@@ -26,6 +26,8 @@ SEG_CUT = 2
 OPT_REF_IDS = 1
 OPT_CUTS_ONLY = 2
 OPT_CTEXT_IN_PLACE = 4
+SCAN_SKIPPED_FIRST_MIN = 1
+SCAN_SKIPPED_CUTS = 2
 
 # Every exported symbol of include/pfscdc.h (checked by tests/test_abi.py).
 EXPORTED = [
@@ -51,6 +53,7 @@ EXPORTED = [
     "pfscdc_merge_file_hash", "pfscdc_last_create_timings", "pfscdc_writer_prefetch",
     "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
     "pfscdc_last_kernel_spans", "pfscdc_last_kernel_clocks", "pfscdc_order_hash_after",
+    "pfscdc_set_knob", "pfscdc_get_knob", "pfscdc_knob_info", "pfscdc_last_scan_mode",
 ]
 
 
@@ -183,6 +186,10 @@ def load() -> C.CDLL:
             "pfscdc_debug_candidates": (u64, [vp, P(u64), u64]),
             "pfscdc_last_timings": (i32, [vp, P(C.c_float)]),
             "pfscdc_last_scan_bytes": (i32, [vp, P(u64)]),
+            "pfscdc_last_scan_mode": (i32, [vp, P(u32)]),
+            "pfscdc_set_knob": (i32, [C.c_char_p, i64]),
+            "pfscdc_get_knob": (i32, [C.c_char_p, P(i64)]),
+            "pfscdc_knob_info": (C.c_char_p, [i32, P(i64), P(i64), P(i64)]),
             "pfscdc_last_kernel_spans": (i32, [vp, P(C.c_float)]),
             "pfscdc_last_kernel_clocks": (i32, [vp, P(C.c_float)]),
             "pfscdc_set_options": (i32, [vp, u32]),
@@ -261,3 +268,53 @@ def go_int63(seed: int, n: int) -> list[int]:
     if rc:
         raise PfsCdcError(rc, "pfscdc_go_int63")
     return list(out)
+
+
+# ---- tuning knobs (pfscdc.h: process-wide integers named after their PFSCDC_* variables) ----
+
+def knob_info() -> dict[str, tuple[int, int, int]]:
+    """Every knob the library has: name -> (lo, hi, default)."""
+    lib = load()
+    out = {}
+    i = 0
+    while True:
+        lo, hi, d = C.c_int64(), C.c_int64(), C.c_int64()
+        name = lib.pfscdc_knob_info(i, C.byref(lo), C.byref(hi), C.byref(d))
+        if name is None:
+            return out
+        out[name.decode()] = (lo.value, hi.value, d.value)
+        i += 1
+
+
+def get_knob(name: str) -> int:
+    v = C.c_int64()
+    rc = load().pfscdc_get_knob(name.encode(), C.byref(v))
+    if rc:
+        raise PfsCdcError(rc, f"unknown knob {name}")
+    return v.value
+
+
+def set_knob(name: str, value: int) -> None:
+    rc = load().pfscdc_set_knob(name.encode(), int(value))
+    if rc:
+        raise PfsCdcError(rc, f"knob {name}={value}: unknown name or out of range")
+
+
+class knobs:
+    """Context manager: set knobs for the block, restore them after.
+    ``with knobs(PFSCDC_SCAN_GRID=1): ...``"""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = get_knob(k)
+            set_knob(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_knob(k, v)
+        return False

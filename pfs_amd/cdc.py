@@ -381,6 +381,13 @@ class Chunker:
         self._check(self.lib.pfscdc_last_scan_bytes(self.ctx, C.byref(v)), "last_scan_bytes")
         return int(v.value)
 
+    def last_scan_mode(self) -> int:
+        """The skipping the last scan did (pfscdc_last_scan_mode): bit 1 the first min - 1
+        bytes of each file, bit 2 past the cuts it settled (_lib.SCAN_SKIPPED_*)."""
+        v = C.c_uint32(0)
+        self._check(self.lib.pfscdc_last_scan_mode(self.ctx, C.byref(v)), "last_scan_mode")
+        return int(v.value)
+
     def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
         out = (C.c_uint64 * cap)()
         n = self.lib.pfscdc_debug_candidates(self.ctx, out, cap)

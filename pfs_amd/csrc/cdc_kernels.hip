@@ -344,74 +344,6 @@ static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block
       record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec, plan);  \
   }
 
-// --- the pair form of the g-recurrence (PAIR, narrow masks): two positions per 64-bit rotation --
-// g_{t+1} = rotl(g_{t-1}, 2) ^ rotl(T[x_t], 1) ^ T[x_{t+1}], so with 16-byte table entries
-// {T, R = rotl(T, 1)} (16 copies, entry idx of copy c at idx * 256 + c * 16: every 16-lane group
-// of a ds_read_b128 conflict free with c = lane & 15) a pair of positions costs one 64-bit
-// rotation by 2 (two v_alignbit_b32) and only the low word of the intermediate g_t (one
-// v_alignbit_b32): 11 VALU per pair (2 v_perm_b32 addresses, 3 v_alignbit_b32, 2 v_bitop3_b32
-// XOR3s for the keys' inputs, 2 XORs, 1 XOR3 for the high word, 1 v_min3_u32) instead of 13.
-// The even position reads its whole entry (ds_read_b128), the odd one T alone (ds_read_b64 at
-// the same 16-copy layout: lanes l and l + 16 share a copy, 2-way on that read).  16 copies of
-// 16 B = the same 64 KiB of LDS as the one-position form's 32 copies of 8 B.
-#ifndef PFS_EXP_PAHEAD
-#define PFS_EXP_PAHEAD 5
-#endif
-constexpr bool kScanPairDefault = false;  // A/B until measured
-constexpr int kPAhead = PFS_EXP_PAHEAD;  // pairs of lookups in flight (two ds_reads each)
-static_assert(kPAhead >= 1 && 2 * kPAhead - 1 <= 15, "lgkmcnt is 4 bits");
-
-PFS_DEV u32x4 lds_read_b128_async(uint32_t a) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-
-#define PFS_ROLL64P(IN, POS)                                                              \
-  {                                                                                       \
-    uint32_t acc = 0xffffffffu;                                                           \
-    u32x4 ea_[kPAhead];                                                                   \
-    uint64_t eb_[kPAhead];                                                                \
-    StaticFor<0, kPAhead>::run([&](auto pc) {                                             \
-      constexpr int t = 2 * decltype(pc)::value;                                          \
-      ea_[t / 2] = lds_read_b128_async(tab_addr(IN[t >> 2], lane_off, t & 3));            \
-      eb_[t / 2] = lds_read_async(tab_addr(IN[(t + 1) >> 2], lane_off, (t + 1) & 3));     \
-    });                                                                                   \
-    StaticFor<0, 32>::run([&](auto pc) {                                                  \
-      constexpr int p = decltype(pc)::value, t = 2 * p;                                   \
-      /* pairs in flight: p .. min(p+K-1, 31); wait until only the younger ones remain */  \
-      constexpr int inflight = (32 - p < kPAhead) ? 32 - p : kPAhead;                     \
-      __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (inflight - 1)) << 8));                   \
-      __builtin_amdgcn_sched_barrier(0);                                                  \
-      /* all four words stay allocated until the read retires (T_hi is unused: left to */ \
-      /* itself the compiler reuses its register while the ds_read_b128 is in flight) */  \
-      asm volatile("" : "+v"(ea_[p % kPAhead]));                                          \
-      const u32x4 a_ = ea_[p % kPAhead];                                                  \
-      const uint64_t b_ = eb_[p % kPAhead];                                               \
-      const uint32_t l0_ = __builtin_amdgcn_alignbit(hl, hh, 31);                         \
-      const uint32_t k0_ = xor3(l0_, a_.x, ring[t]);                                      \
-      ring[t] = l0_ ^ a_.x;                                                               \
-      asm volatile("" : "+v"(ring[t])); /* computed now: frees l0_ and the entry */       \
-      const uint32_t r2l_ = __builtin_amdgcn_alignbit(hl, hh, 30);                        \
-      const uint32_t r2h_ = __builtin_amdgcn_alignbit(hh, hl, 30);                        \
-      const uint32_t n1_ = xor3(r2l_, a_.z, (uint32_t)b_);                                \
-      const uint32_t k1_ = n1_ ^ ring[t + 1];                                             \
-      ring[t + 1] = n1_;                                                                  \
-      hl = n1_;                                                                           \
-      hh = xor3(r2h_, a_.w, (uint32_t)(b_ >> 32));                                        \
-      acc = acc < k0_ ? acc : k0_; /* one v_min3_u32 with the next line */                \
-      acc = acc < k1_ ? acc : k1_;                                                        \
-      __builtin_amdgcn_sched_barrier(0);                                                  \
-      if constexpr (p + kPAhead < 32) {                                                   \
-        constexpr int u = t + 2 * kPAhead;                                                \
-        ea_[p % kPAhead] = lds_read_b128_async(tab_addr(IN[u >> 2], lane_off, u & 3));    \
-        eb_[p % kPAhead] = lds_read_async(tab_addr(IN[(u + 1) >> 2], lane_off, (u + 1) & 3)); \
-      }                                                                                   \
-    });                                                                                   \
-    if (__builtin_expect(acc < cand_thr, 0))                                              \
-      record_block_g(data, tail, n_main, (POS), n, tile_base, mask64, table, rec, plan);  \
-  }
-
 // Data staging: a wave owns 64 strips (lane l <-> strip l, kStrip bytes each) and walks
 // them 128 bytes at a time.  Per step, 8 LDS-DMA instructions (global_load_lds_dwordx4)
 // each fetch one full 128-byte line from 8 strips (8 lines per instruction: the coalesced
@@ -474,9 +406,8 @@ PFS_DEV void scan_unit_plan(const ScanPlan* __restrict__ plan, uint64_t slot, ui
   unit = sl.x;
   const uint32_t f = sl.y, rank = sl.z >> 8;
   skip = sl.z & 0xffu;
-  const uint32_t mode = plan->mode;
-  fr = mode == 3 ? ~0u : f | (rank < 255 ? rank : 255u) << 24;
-  if (rank == 0 || mode != 1) return;  // nothing of the file before this unit (or A/B forms)
+  fr = f | (rank < 255 ? rank : 255u) << 24;
+  if (rank == 0) return;  // nothing of the file before this unit
   const uint32_t v = __hip_atomic_fetch_or(plan->rslots + (uint64_t)f * kRankSlots + lane, 0u,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t fs = plan->offs[f], fe = plan->offs[f + 1];
@@ -535,7 +466,7 @@ PFS_DEV void scan_unit_report(const ScanPlan* __restrict__ plan, uint32_t fr, ui
                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool WIDE, bool PAIR>
+template <bool WIDE>
 __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kScanWaves / 4, kScanWaves / 4))) void cdc_scan_kernel(
     const uint8_t* __restrict__ data, const uint8_t* __restrict__ tail, uint64_t n,
     const uint64_t* __restrict__ table, uint32_t kshift, uint64_t mask64, uint64_t ntiles,
@@ -549,29 +480,17 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t n_main = n & ~63ULL;
 
-  if constexpr (PAIR) {
-    // {T, rotl(T, 1)} replicated: entry idx of copy c at byte idx*256 + c*16 (PFS_ROLL64P)
-    for (int i = threadIdx.x; i < 256 * 16; i += kScanBlock) {
-      const int idx = i >> 4, c = i & 15;
-      const uint64_t t0 = table[idx];
-      const uint64_t v = kshift == 0 ? t0 : (t0 << kshift) | (t0 >> (64 - kshift));
-      uint64_t* e = reinterpret_cast<uint64_t*>(smem + idx * 256 + c * 16);
-      e[0] = v;
-      e[1] = rotl1_64(v);
-    }
-  } else {
-    // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
-    for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
-      const int idx = i >> 5, c = i & 31;
-      // narrow masks roll in a frame rotated left by kshift = 32 - bits (see PFS_ROLL64G)
-      const uint64_t v = table[idx];
-      reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
-          WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
-    }
+  // T replicated: entry idx of copy c at byte idx*256 + c*8 -> banks {2c, 2c+1}.
+  for (int i = threadIdx.x; i < 256 * 32; i += kScanBlock) {
+    const int idx = i >> 5, c = i & 31;
+    // narrow masks roll in a frame rotated left by kshift = 32 - bits (see PFS_ROLL64G)
+    const uint64_t v = table[idx];
+    reinterpret_cast<uint64_t*>(smem)[idx * 32 + c] =
+        WIDE || kshift == 0 ? v : (v << kshift) | (v >> (64 - kshift));
   }
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t lane_off = PAIR ? (lane & 15u) * 16u : (lane & 31u) * 8u;
+  const uint32_t lane_off = (lane & 31u) * 8u;
   uint8_t* wbuf = smem + kTableLdsBytes + wave * kStageBytes;
   const uint32_t rd_base = lane * 128u;
   const uint32_t swz_l = stage_swz(lane);
@@ -692,9 +611,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
           if constexpr (WIDE) {
             PFS_ROLL64(c0, prv, pos)
             if (pos + 64 < n) PFS_ROLL64(c1, c0, pos + 64)
-          } else if constexpr (PAIR) {
-            PFS_ROLL64P(c0, pos)
-            if (pos + 64 < n) PFS_ROLL64P(c1, pos + 64)
           } else {
             PFS_ROLL64G(c0, pos)
             if (pos + 64 < n) PFS_ROLL64G(c1, pos + 64)
@@ -779,12 +695,17 @@ __global__ __launch_bounds__(256) void scan_skip_kernel(
           break;
         }
       }
+      // A unit crowded with more than 64 file starts and no tracked file: with a plan
+      // (min - 1 >= one unit) it has no eligible position at all -- every file past the first
+      // starts after ub, so its first eligible position lies past ue -- and it must not take a
+      // dispatch slot scan_slots_kernel would never fill.
+      if (uinfo && tf == ~0u) s = kAll;
       if (s < kAll && ub + s * kStep >= ue) s = kAll;
       if (s < kAll) live = ue - (ub + s * kStep);
     }
     skip[u] = s;
     if (uinfo) {
-      const bool scanned_unit = s < kAll;
+      const bool scanned_unit = s < kAll;  // implies tf != ~0u
       uinfo[2 * u] = scanned_unit ? tf : ~0u;
       uinfo[2 * u + 1] = s | (rank < 255 ? rank : 255u) << 8;
       if (scanned_unit) atomicAdd(&s_hist[rank < kPlanBuckets - 1 ? rank : kPlanBuckets - 1], 1u);
@@ -1568,7 +1489,9 @@ PFS_DEV void fold_diag(uint64_t& ha, uint64_t& hb, uint64_t a, uint64_t b, uint6
 constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
 // Development trace (PFSCDC_WAVE_TRACE, timing only): per hash wave its end time and its
 // hardware slot (HW_ID, XCC_ID), to read how the launch drains.  nullptr: off.
+#ifdef PFS_WAVE_TRACE
 __device__ uint64_t* g_wave_trace = nullptr;
+#endif
 template <int MODE>
 __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
@@ -1620,10 +1543,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   const uint64_t t_mask = j == 0 ? ~0ULL : 0ULL;  // the byte counter t goes into v[12] (lane 0)
   const uint64_t h0b = iv_d;
 
-  if ((prio_blocks >> 31) && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // A/B: static
-  if ((prio_blocks & 0x3fffffffu) == 0x3fffffffu)  // auto: only when quads refill
-    prio_blocks = (prio_blocks & 0xc0000000u) |
-                  (nseg > (uint64_t)gridDim.x * (kHashBlock / 4) ? 8192u : 0u);
+  if (prio_blocks == kHashPrioAuto)  // only when quads refill
+    prio_blocks = nseg > (uint64_t)gridDim.x * (kHashBlock / 4) ? 8192u : 0u;
   bool active = false;   // this quad holds a segment
   uint32_t bin_next = kNoNext;  // hash bins: the quad's next segment (its file's following one)
   bool drained = false;  // wave-uniform: the queue is exhausted
@@ -1631,7 +1552,6 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // so the refill ballot, the exit test and the priority ballot are skipped (they cost ~20
   // VALU per block when evaluated every block)
   uint32_t quiet = 0;
-  const bool graded = (prio_blocks & 0x40000000u) != 0;
   uint64_t L = 0, nblk = 0, blk = 0;
   const uint8_t* src = data;
   pfscdc_segment* seg = segs;
@@ -1751,8 +1671,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
   // other alone at the lone-wave rate.  At least every fair_every blocks each wave adds the
   // blocks it ran to a launch-wide counter and raises its issue priority while it is behind
   // the launch's average, so the waves of a SIMD advance together.
-  const uint32_t kFairEvery = (fair_every & 0x7fffffffu) ? (fair_every & 0x7fffffffu) : 256;
-  const bool fair_graded = (fair_every >> 31) != 0;
+  const uint32_t kFairEvery = fair_every ? fair_every : 256;
   uint32_t wave_steps = 0;  // blocks this wave ran (wave-uniform; fair share, the trace)
   uint32_t reported = 0;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kHashBlock / 64);
@@ -1839,20 +1758,12 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tot);
         reported = wave_steps;
         const uint64_t mine = (uint64_t)wave_steps * nwaves, all = tot + d;
-        if (fair_graded && mine + 2ull * kFairEvery * nwaves < all) __builtin_amdgcn_s_setprio(2);
-        else if (mine < all) __builtin_amdgcn_s_setprio(1);
+        if (mine < all) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
-      } else if (prio_blocks & 0x3fffffffu) {  // waves holding a long chain issue first
-        const uint64_t T = prio_blocks & 0x3fffffffu, rem = active ? nblk - blk : 0;
-        if (prio_blocks & 0x40000000u) {  // graded: 3 above 2T, 2 above T, 1 above T/2
-          if (__ballot(rem > 2 * T)) __builtin_amdgcn_s_setprio(3);
-          else if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
-          else if (__ballot(rem > T / 2)) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
-        } else {
-          if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
-          else __builtin_amdgcn_s_setprio(0);
-        }
+      } else if (prio_blocks) {  // waves holding a long chain issue first
+        const uint64_t T = prio_blocks, rem = active ? nblk - blk : 0;
+        if (__ballot(rem > T)) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
       }
 
       // next event: the step after the first active quad's last block, or the step at which
@@ -1861,13 +1772,10 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       const uint32_t rem = rem64 > 0xffffffffULL ? 0xffffffffu : (uint32_t)rem64;
       uint32_t q = wave_min_u32(active ? rem : 0xffffffffu) - 1;
       if (fair && q > kFairEvery - 1) q = kFairEvery - 1;
-      if (!fair && (prio_blocks & 0x3fffffffu)) {
-        // the next block at which the longest chain left crosses a priority threshold
-        const uint32_t T = prio_blocks & 0x3fffffffu, rmax = wave_max_u32(rem);
-        const uint32_t th[3] = {graded ? 2 * T : T, T, T / 2};
-#pragma unroll
-        for (int i = 0; i < (graded ? 3 : 1); i++)
-          if (rmax > th[i] && rmax - th[i] - 1 < q) q = rmax - th[i] - 1;
+      if (!fair && prio_blocks) {
+        // the next block at which the longest chain left crosses the priority threshold
+        const uint32_t T = prio_blocks, rmax = wave_max_u32(rem);
+        if (rmax > T && rmax - T - 1 < q) q = rmax - T - 1;
       }
       quiet = q;
     }
@@ -1967,6 +1875,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       }
     }
   }
+#ifdef PFS_WAVE_TRACE
   if (MODE == kModeHash && g_wave_trace && lane == 0) {
     const uint64_t w = (uint64_t)blockIdx.x * (kHashBlock / 64) + (threadIdx.x >> 6);
     const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
@@ -1976,9 +1885,11 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     g_wave_trace[4 * w + 2] = wave_steps;
     g_wave_trace[4 * w + 3] = __builtin_amdgcn_s_memtime() - span_clk.t0;  // shader cycles
   }
+#endif
   span_end(span, span_clk);
 }
 
+#ifdef PFS_WAVE_TRACE
 hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {
   // stream-ordered and synchronous w.r.t. the host value (a development tool: the copy
   // source must outlive the call)
@@ -1986,6 +1897,7 @@ hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {
   if (e != hipSuccess) return e;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_trace), &p, sizeof p, 0, hipMemcpyHostToDevice);
 }
+#endif
 
 // 5d. ChaCha20 ciphertext of whole chunks, one lane per 64-byte keystream block (the Ref.Id
 // pass split in two for chunk lists that cannot fill the GPU, see create_refs_device).  Every
@@ -2001,84 +1913,18 @@ PFS_DEV uint32_t rotl32v(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x
     x[a] += x[b]; x[d] = rotl32v(x[d] ^ x[a], 8);   \
     x[c] += x[d]; x[b] = rotl32v(x[b] ^ x[c], 7);   \
   } while (0)
-__global__ __launch_bounds__(256) void chacha_xor_kernel(
-    const uint8_t* data, const uint64_t* __restrict__ offs,
-    const pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ blk_base, uint32_t n,
-    const pfscdc_ref* __restrict__ refs, uint8_t* out, uint32_t prio) {
-  if (prio) __builtin_amdgcn_s_setprio(2);  // the long chunk set's pass issues first
-  const uint64_t nblocks = blk_base[n];
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  // wave-uniform window of 64 consecutive blocks: the record of its first block by a scalar
-  // binary search, then each lane steps forward over the (rare) record ends in the window
-  const uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x +
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
-  for (uint64_t g0 = w0; g0 < nblocks; g0 += stride) {
-    uint32_t lo = 0, hi = n;  // the last r with blk_base[r] <= g0
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (blk_base[mid] <= g0) lo = mid;
-      else hi = mid;
-    }
-    const uint64_t g = g0 + lane;
-    if (g >= nblocks) continue;
-    while (blk_base[lo + 1] <= g) lo++;
-    const pfscdc_segment& sg = segs[lo];
-    const uint64_t b = g - blk_base[lo];
-    const uint64_t at = offs[sg.file] + sg.offset + 64 * b;
-    const int64_t avail = (int64_t)(sg.size - 64 * b);
-    const uint4 k0 = reinterpret_cast<const uint4*>(refs[lo].dek)[0];
-    const uint4 k1 = reinterpret_cast<const uint4*>(refs[lo].dek)[1];
-    const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                            k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w,
-                            (uint32_t)b, 0u, 0u, 0u};
-    uint32_t x[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) x[i] = s[i];
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-      PFS_CQR(0, 4, 8, 12);
-      PFS_CQR(1, 5, 9, 13);
-      PFS_CQR(2, 6, 10, 14);
-      PFS_CQR(3, 7, 11, 15);
-      PFS_CQR(0, 5, 10, 15);
-      PFS_CQR(1, 6, 11, 12);
-      PFS_CQR(2, 7, 8, 13);
-      PFS_CQR(3, 4, 9, 14);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) x[i] += s[i];
-    const uint8_t* src = data + at;
-    uint8_t* dst = out + at;
-    if (avail >= 64) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        uint4 v;
-        __builtin_memcpy(&v, src + 16 * q, 16);
-        v.x ^= x[4 * q];
-        v.y ^= x[4 * q + 1];
-        v.z ^= x[4 * q + 2];
-        v.w ^= x[4 * q + 3];
-        __builtin_memcpy(dst + 16 * q, &v, 16);
-      }
-    } else {  // the chunk's last block: only its own bytes (the next chunk's follow)
-      for (int64_t k = 0; k < avail; k++)
-        dst[k] = src[k] ^ (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
-    }
-  }
-}
-// The same pass with coalesced memory traffic.  Above, lane l XORs its own 64-byte block, so
-// one 16-byte load or store instruction spans 64 blocks (4 KiB, 32 lines); here each lane
-// still computes its block's keystream, parks it in LDS (64 B per lane, 16-byte slots
+// Memory traffic is coalesced.  Were lane l to XOR its own 64-byte block, one 16-byte load or
+// store instruction would span 64 blocks (4 KiB, 32 lines); instead each lane computes its
+// block's keystream, parks it in LDS (64 B per lane, 16-byte slots
 // XOR-rotated by (block >> 1) & 3 so the 8-lane groups of ds_write_b128 and the 16-lane
 // groups of ds_read_b128 are conflict-free), and the wave then walks its 64-block window as
 // 256 consecutive 16-byte pieces: lane l takes pieces l, l + 64, l + 128, l + 192, so one
 // instruction covers 1 KiB of one chunk (8 lines).  A chunk's last, partial block is written
 // byte by byte up to the chunk's end (in place, the next chunk's first block is another
 // lane's).  c4 commit data plane at G = 2, same box, alternating: 369.5-369.9 -> 378.3-378.8
-// GiB/s (profiles/r4/chacha/).  PFSCDC_CHACHA_COALESCED=0: the per-lane form (A/B).
-// data and out are not __restrict__ in either ChaCha20 kernel: in place (PFSCDC_OPT_CTEXT_IN_PLACE)
-// they are the same buffer; every byte is read before the same lane writes it.
+// GiB/s against the per-lane form (profiles/r4/chacha/; that form is no longer built).
+// data and out are not __restrict__: in place (PFSCDC_OPT_CTEXT_IN_PLACE) they are the same
+// buffer; every byte is read before the same lane writes it.
 constexpr int kChachaBlock = 256;
 __global__ __launch_bounds__(kChachaBlock) void chacha_xor_coalesced_kernel(
     const uint8_t* data, const uint64_t* __restrict__ offs,
@@ -2229,6 +2075,7 @@ PFS_DEV void b2_compress_lane(uint64_t (&h)[8], const uint64_t (&x)[16], uint64_
   for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
 }
 
+#if PFS_HASH_LANES == 1  // the one-lane-per-segment form (compile-time A/B only)
 // One 128-byte block for this lane: eight 16-byte loads.
 PFS_DEV void blk_load_full(uint4 (&m)[8], const uint8_t* p) {
 #pragma unroll
@@ -2359,6 +2206,7 @@ __global__ __launch_bounds__(kHashLaneBlock) void blake2b_lane_kernel(
     }
   }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // synthetic data (bench/tests): splitmix64 finalizer of (file << 40 | word) + gamma*(seed+1)
@@ -2435,21 +2283,11 @@ __global__ void synth_kernel(uint8_t* __restrict__ out, const uint64_t* __restri
 // on the ctx's device before any launch; idempotent, so every ctx sets them on its device.
 hipError_t prepare_kernels() {
   const int lds = (int)kScanLdsBytes;
-  hipError_t e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false, false>,
+  hipError_t e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)cdc_scan_kernel<false, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)cdc_scan_kernel<true, false>,
+  return hipFuncSetAttribute((const void*)cdc_scan_kernel<true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-}
-
-// The narrow scan's form: one position per rotation (PFS_ROLL64G, 32 copies of T) or pairs
-// (PFS_ROLL64P, 16 copies of {T, rotl(T, 1)}).  PFSCDC_SCAN_PAIR=0/1, read per launch.
-static bool scan_pair() {
-  const char* e = getenv("PFSCDC_SCAN_PAIR");
-  return e && *e ? atoi(e) != 0 : kScanPairDefault;
 }
 
 hipError_t launch_scan_skip(const uint64_t* offs, uint32_t nfiles, uint64_t n, uint64_t min_chunk,
@@ -2484,16 +2322,12 @@ hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, con
   const size_t lds = kScanLdsBytes;
   const uint64_t mask64 = average_bits >= 64 ? ~0ULL : ((1ULL << average_bits) - 1);
   const ScanPlan* const pl = d_plan;
-  if (average_bits <= 32 && scan_pair())
-    cdc_scan_kernel<false, true><<<grid, kScanBlock, lds, st>>>(
-        data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
-        entries, n_entries, skip, span, pl);
-  else if (average_bits <= 32)
-    cdc_scan_kernel<false, false><<<grid, kScanBlock, lds, st>>>(
+  if (average_bits <= 32)
+    cdc_scan_kernel<false><<<grid, kScanBlock, lds, st>>>(
         data, tail, n, d_table, 32 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
         entries, n_entries, skip, span, pl);
   else
-    cdc_scan_kernel<true, false><<<grid, kScanBlock, lds, st>>>(
+    cdc_scan_kernel<true><<<grid, kScanBlock, lds, st>>>(
         data, tail, n, d_table, 64 - average_bits, mask64, ntiles, recs, unit_ctr, done_ctr,
         entries, n_entries, skip, span, pl);
   return hipGetLastError();
@@ -2535,30 +2369,11 @@ hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_ba
 // queue are issued ahead of the short fill-in work.  It pays when the queue holds more
 // segments than the grid has quads (c2: 44K segments, 32K quads: hash 79 ms vs 96 ms per
 // 128 GiB at 8192 blocks = 1 MiB; 6000-10000 within 1%, graded levels and a static
-// block-parity priority worse) and costs ~4% when every segment starts at once (c4: 132 vs
-// 127 ms), so the default ("auto") enables it at 8192 only when quads will refill
-// (tools/ab_prio*.sh, profiles/r1_prio/).  Knobs: PFSCDC_HASH_PRIO (0 = off, N = fixed),
-// PFSCDC_HASH_PRIO_GRADED, PFSCDC_HASH_PRIO_STATIC (A/B only).
-constexpr uint32_t kHashPrioBlocks = 0x3fffffffu;  // auto
-static uint32_t hash_prio_blocks() {
-  static const uint32_t v = [] {
-    const char* e = getenv("PFSCDC_HASH_PRIO");
-    const char* m = getenv("PFSCDC_HASH_PRIO_STATIC");
-    const char* g = getenv("PFSCDC_HASH_PRIO_GRADED");
-    return (e ? (uint32_t)atoi(e) : kHashPrioBlocks) | (m && atoi(m) ? 0x80000000u : 0u) |
-           (g && atoi(g) ? 0x40000000u : 0u);
-  }();
-  return v;
-}
-
-// PFSCDC_HASH_FAIR_EVERY: blocks between a fair-share wave's priority updates (default 256);
-// PFSCDC_HASH_FAIR_GRADED=1: priority 2 for a wave more than two intervals behind the launch
-// average, 1 behind it, 0 ahead (bit 31 of the kernel argument).  Read per launch.
-static uint32_t hash_fair_every() {
-  const char* e = getenv("PFSCDC_HASH_FAIR_EVERY");
-  const int x = e ? atoi(e) : 0;
-  const char* g = getenv("PFSCDC_HASH_FAIR_GRADED");
-  return (uint32_t)(x >= 8 && x <= 65536 ? x : 256) | (g && atoi(g) ? 0x80000000u : 0u);
+// block-parity priority worse, no longer built) and costs ~4% when every segment starts at
+// once (c4: 132 vs 127 ms), so the default (kHashPrioAuto) enables it at 8192 only when quads
+// will refill (profiles/r1_prio/).
+static uint32_t prio_arg(uint32_t prio) {
+  return prio == kHashPrioNone ? 0u : prio ? prio : kHashPrioAuto;
 }
 
 // Waves per SIMD for a hash launch.  One quad runs a chain's 128-B blocks strictly in order,
@@ -2566,10 +2381,9 @@ static uint32_t hash_fair_every() {
 // down (the two share the issue slots).  One wave per SIMD when the launch is bound by its
 // longest chain even then (longest blocks >= total blocks / the quads of one wave per SIMD:
 // c3, c4, a single configs[1] batch, most chunk.Create passes), two otherwise (c2's 128 GiB
-// steps: 72 vs 80 ms; c4: 100 vs 104-110 ms).  PFSCDC_HASH_WAVES=n forces n (A/B).
-int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus) {
-  const char* e = getenv("PFSCDC_HASH_WAVES");  // read per launch (tests switch it)
-  const int forced = e ? atoi(e) : 0;
+// steps: 72 vs 80 ms; c4: 100 vs 104-110 ms).  forced (the PFSCDC_HASH_WAVES knob) in 1..8
+// overrides it.
+int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus, int forced) {
   if (forced >= 1 && forced <= 8) return forced;
   const uint64_t quads1 = (uint64_t)num_cus * 4 * (64 / 4);
   const uint64_t longest = (longest_bytes + 127) / 128, total = total_bytes / 128;
@@ -2588,9 +2402,11 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered, uint64_t* span, int waves, uint32_t prio,
-                          bool cu_exclusive, const uint32_t* next, uint64_t* fair) {
+                          bool cu_exclusive, const uint32_t* next, uint64_t* fair,
+                          uint32_t fair_every) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
+#if PFS_HASH_LANES == 1
   if (kHashLanesPerSegment == 1) {
     const uint64_t need = (max_segments + kHashLaneBlock - 1) / kHashLaneBlock;
     const uint64_t full = (uint64_t)num_cus * 4 * (waves > 0 ? waves : kHashWavesPerSimd) /
@@ -2600,6 +2416,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                                                                    order, counter, nbytes);
     return hipGetLastError();
   }
+#endif
   // cu_exclusive: 64 KiB of unused dynamic LDS on top of the 20 KiB message buffers, so no
   // two workgroups (of this or of another launch) share a CU.  A chain-bound launch at one
   // wave per SIMD has one workgroup per CU anyway; the reservation keeps a second such launch
@@ -2608,8 +2425,7 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
   const size_t dyn = cu_exclusive ? 64u * 1024u : 0u;
   blake2b_kernel<kModeHash><<<hash_grid(max_segments, num_cus, waves), kHashBlock, dyn, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, nullptr, nullptr,
-      prio ? prio : hash_prio_blocks(), span, ordered ? next : nullptr,
-      ordered ? fair : nullptr, hash_fair_every());
+      prio_arg(prio), span, ordered ? next : nullptr, ordered ? fair : nullptr, fair_every);
   return hipGetLastError();
 }
 
@@ -2630,7 +2446,7 @@ hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segm
       segs, nsegs ? nsegs : seg_count, refs, counter);
   blake2b_kernel<kModeRefId><<<hash_grid(max_segments, num_cus, waves), kHashBlock, 0, st>>>(
       data, offs, segs, seg_count, order, counter, nbytes, refs, ctext_out,
-      prio ? prio : hash_prio_blocks(), nullptr, next, nullptr, 0u);
+      prio_arg(prio), nullptr, next, nullptr, 0u);
   return hipGetLastError();
 }
 
@@ -2651,13 +2467,8 @@ hipError_t launch_chacha_xor(const uint8_t* data, const uint64_t* offs, const pf
   const uint64_t need = (nblocks + 255) / 256,
                  full = (uint64_t)num_cus * (one_wave_per_simd ? 1 : 32);
   const unsigned grid = (unsigned)(need < full ? need : full);
-  const char* e = getenv("PFSCDC_CHACHA_COALESCED");  // read per launch (tests switch it)
-  if (!(e && *e && atoi(e) == 0))
-    chacha_xor_coalesced_kernel<<<grid, kChachaBlock, 0, st>>>(data, offs, segs, blk_base, n,
-                                                              refs, out, prio ? 1u : 0u);
-  else
-    chacha_xor_kernel<<<grid, 256, 0, st>>>(data, offs, segs, blk_base, n, refs, out,
-                                            prio ? 1u : 0u);
+  chacha_xor_coalesced_kernel<<<grid, kChachaBlock, 0, st>>>(data, offs, segs, blk_base, n,
+                                                            refs, out, prio ? 1u : 0u);
   return hipGetLastError();
 }
 
@@ -2668,8 +2479,8 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
   if (nsegs == 0) return hipSuccess;
   hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
   blake2b_kernel<kModeGet><<<hash_grid(nsegs, num_cus, waves), kHashBlock, 0, st>>>(
-      ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, hash_prio_blocks(),
-      nullptr, nullptr, nullptr, 0u);
+      ctext, offs, segs, seg_count, order, counter, nbytes, refs, ptext, prio_arg(0), nullptr,
+      nullptr, nullptr, 0u);
   return hipGetLastError();
 }
 

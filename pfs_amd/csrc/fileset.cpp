@@ -197,15 +197,11 @@ namespace {
 // Contexts the writers make for themselves (a second group writer's data ctx, one ctx per
 // index level) are kept for the next writer: a ctx owns its stream, events and grow-only
 // device staging (a group write's whole input), so making them per commit costs more than
-// the commit's small index streams.  Keyed by (device, params, options); at most
-// PFSCDC_CTX_CACHE of them (default 32; 0 turns the cache off).
+// the commit's small index streams.  Keyed by (device, params, options); at most the
+// PFSCDC_CTX_CACHE knob's count of them (default 32; 0 turns the cache off).
 struct CtxCache {
   std::mutex mu;
   std::vector<std::pair<std::string, pfscdc_ctx*>> free;
-  size_t cap = [] {
-    const char* e = getenv("PFSCDC_CTX_CACHE");
-    return e ? (size_t)std::max(0, atoi(e)) : (size_t)32;
-  }();
   static std::string key(const pfscdc_params& p, int device, uint32_t options) {
     char b[160];
     snprintf(b, sizeof b, "%d/%u/%lld/%lld/%lld/%u", device, p.average_bits, (long long)p.seed,
@@ -249,7 +245,7 @@ struct CtxCache {
   void give(pfscdc_ctx* c) {
     if (!c) return;
     std::unique_lock<std::mutex> lk(mu);
-    if (free.size() < cap) {
+    if (free.size() < (size_t)pfscdc::knob(pfscdc::Knob::CtxCache)) {
       free.emplace_back(key(pfscdc::ctx_params(c), pfscdc::ctx_device(c), pfscdc::ctx_options(c)), c);
       return;
     }
@@ -597,8 +593,8 @@ struct Arena {
 // memcpy split over threads for large Puts (one core copies ~10 GB/s).  The threads are
 // persistent: a Put is typically one file of ~10 MB, and spawning 15 threads per Put cost
 // more than the copy (c4: 30-40 GB/s with spawned threads).
-// PFSCDC_COPY_THREADS, else the job's thread share (OMP_NUM_THREADS: 16 per GPU on the MI355X
-// pool, whose nproc shows the whole machine), else up to 16 hardware threads.
+// The PFSCDC_COPY_THREADS knob (read when the first large Put copies), else up to 16 hardware
+// threads (the job's share on the MI355X pool: 16 per GPU, whose nproc shows the whole machine).
 class CopyPool {
  public:
   static CopyPool& get() {
@@ -642,9 +638,7 @@ class CopyPool {
   CopyPool() {
     const unsigned hw = std::thread::hardware_concurrency();
     unsigned t = std::min(16u, hw ? hw : 1u);
-    if (const char* e = getenv("PFSCDC_COPY_THREADS")) t = (unsigned)std::max(1, atoi(e));
-    else if (const char* e2 = getenv("OMP_NUM_THREADS"))
-      if (atoi(e2) > 0) t = (unsigned)atoi(e2);
+    if (const int64_t k = pfscdc::knob(pfscdc::Knob::CopyThreads)) t = (unsigned)k;
     for (unsigned i = 1; i < t; i++) workers_.emplace_back([this] { run(); });
     for (auto& w : workers_) w.detach();
   }
@@ -681,20 +675,13 @@ void copy_parallel(uint8_t* dst, const uint8_t* src, uint64_t n) { CopyPool::get
 // page-locking 1 GB for every fileset of every commit (hipHostMalloc) costs more than the Put
 // copies themselves.  Process-wide pool, capped by BYTES (each pooled arena holds its host
 // bytes page-locked and, with the device mirror, as many bytes of HBM):
-// PFSCDC_UW_ARENA_POOL_BYTES, default 40e9 (one 32 GiB group's worth of 1e9-byte arenas, so a
-// group never page-locks fresh ones; a 16-arena pool re-allocated 18 of them every commit,
-// 11.7 vs 27.8 GiB/s, profiles/r3/uw_groups/).  PFSCDC_UW_ARENA_POOL (a count of 1e9-byte
-// arenas) is still read when the byte form is unset.  pfscdc_uw_trim_cache() frees the pool.
+// the PFSCDC_UW_ARENA_POOL_BYTES knob, default 40e9 (one 32 GiB group's worth of 1e9-byte
+// arenas, so a group never page-locks fresh ones; a 16-arena pool re-allocated 18 of them every
+// commit, 11.7 vs 27.8 GiB/s, profiles/r3/uw_groups/).  pfscdc_uw_trim_cache() frees the pool.
 struct ArenaPool {
   std::mutex mu;
   std::vector<std::unique_ptr<Arena>> free;
   uint64_t held = 0;  // bytes of the pooled arenas (host; the mirrors hold as many on devices)
-  uint64_t cap_bytes = []() -> uint64_t {
-    if (const char* e = getenv("PFSCDC_UW_ARENA_POOL_BYTES")) return (uint64_t)std::max(0LL, atoll(e));
-    if (const char* e = getenv("PFSCDC_UW_ARENA_POOL"))
-      return (uint64_t)std::max(0, atoi(e)) * 1000000000ull;
-    return 40000000000ull;
-  }();
   std::unique_ptr<Arena> take(uint64_t bytes, int device) {
     std::lock_guard<std::mutex> lk(mu);
     for (size_t i = free.size(); i-- > 0;)
@@ -709,7 +696,7 @@ struct ArenaPool {
   }
   void give(std::unique_ptr<Arena> a) {
     std::unique_lock<std::mutex> lk(mu);
-    if (held + a->cap <= cap_bytes) {
+    if (held + a->cap <= (uint64_t)pfscdc::knob(pfscdc::Knob::UwArenaPoolBytes)) {
       held += a->cap;
       free.push_back(std::move(a));
       return;
@@ -775,11 +762,6 @@ struct GroupWorker {
   double stage_ms[8] = {};  // close_group's 6 stages, [6] the index writers, [7] group wall
 };
 
-static bool index_grouped() {
-  const char* e = getenv("PFSCDC_UW_INDEX_GROUPED");
-  return !(e && *e && atoi(e) == 0);
-}
-
 struct pfscdc_uwriter {  // unordered_writer.go:15-26
   int64_t mem_threshold = 1000000000;
   int64_t mem_available = 1000000000;
@@ -791,7 +773,7 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   // one of the group writers, round robin, while Puts continue.  The output equals
   // serializing one at a time; each fileset's chunk stream is independent.  A group's GPU
   // time is bound by its longest chunks' two serial chains (~340 ms on c4) whatever its size,
-  // so groups are large: 32 GiB (PFSCDC_UW_INFLIGHT; c4, 32 GiB Put: 8 GiB groups 18.8, 16
+  // so groups are large: 32 GiB (the PFSCDC_UW_INFLIGHT knob; c4, 32 GiB Put: 8 GiB groups 18.8, 16
   // GiB 25.1, 32 GiB 27.8 GiB/s, profiles/r3/uw_groups/).
   std::vector<Buffer> pending;
   std::vector<std::unique_ptr<Arena>> pool;  // arenas of written filesets, for reuse
@@ -808,10 +790,8 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   }
   double put_copy_ms = 0;  // host copies of the Puts into the arenas
   int device = 0;
-  bool mirror = [] {  // PFSCDC_UW_MIRROR=0: upload at group write time instead (A/B)
-    const char* e = getenv("PFSCDC_UW_MIRROR");
-    return !(e && atoi(e) == 0);
-  }();
+  bool mirror = true;  // the PFSCDC_UW_MIRROR knob (0: upload at group write time instead)
+  bool index_grouped = true;  // the PFSCDC_UW_INDEX_GROUPED knob (0: one fileset at a time)
   hipStream_t up_stream = nullptr;  // the Puts' uploads into the arena mirrors
   uint64_t pending_bytes = 0, inflight_bytes = 32ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
@@ -916,8 +896,8 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
       rc = pfscdc::writers_close_group(cws.data(), cws.size(), gw.stage_ms, evs.data(), evs.size());
     const auto g1 = clk::now();
     // the indexes of every fileset of the group, closed level by level in grouped closes
-    // (PFSCDC_UW_INDEX_GROUPED=0: one fileset at a time, A/B)
-    if (index_grouped()) {
+    // (the PFSCDC_UW_INDEX_GROUPED knob at 0: one fileset at a time)
+    if (index_grouped) {
       std::vector<IndexWriter*> iws;
       for (size_t i = 0; i < fws.size() && !rc; i++) {
         rc = fws[i]->finish_last_entry();
@@ -1058,10 +1038,9 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
     ip.seed = 0;
   }
   // group writers: the first on the caller's data ctx, the others on ctxs of their own
-  // (PFSCDC_UW_WORKERS, default 1: two groups in flight contend for the CUs, and each group's
-  // chunk.Create chains then run longer; c4, 8 GiB: 15.2 GiB/s with one, 8.9 with two)
-  int nworkers = 1;
-  if (const char* e = getenv("PFSCDC_UW_WORKERS")) nworkers = std::max(1, std::min(8, atoi(e)));
+  // (the PFSCDC_UW_WORKERS knob, default 1: two groups in flight contend for the CUs, and each
+  // group's chunk.Create chains then run longer; c4, 8 GiB: 15.2 GiB/s with one, 8.9 with two)
+  const int nworkers = (int)pfscdc::knob(pfscdc::Knob::UwWorkers);
   for (int k = 0; k < nworkers; k++) {
     auto gw = std::make_unique<GroupWorker>();
     gw->st.cb = cb;
@@ -1084,7 +1063,9 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
   }
   w->device = pfscdc::ctx_device(data_ctx);
   if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
-  if (const char* e = getenv("PFSCDC_UW_INFLIGHT")) w->inflight_bytes = strtoull(e, nullptr, 10);
+  w->inflight_bytes = (uint64_t)pfscdc::knob(pfscdc::Knob::UwInflight);
+  w->mirror = pfscdc::knob(pfscdc::Knob::UwMirror) != 0;
+  w->index_grouped = pfscdc::knob(pfscdc::Knob::UwIndexGrouped) != 0;
   *out = w;
   return PFSCDC_OK;
 }

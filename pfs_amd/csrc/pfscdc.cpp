@@ -93,9 +93,12 @@ struct pfscdc_ctx {
   DevBuf<uint4> d_uslots;
   DevBuf<uint32_t> d_rslots;
   DevBuf<ScanPlan> d_planhdr;  // the scan kernel's view of the plan (scan_slots_kernel stores it)
-  DevBuf<uint64_t> d_wtrace;    // PFSCDC_WAVE_TRACE: per hash wave end time + hardware slot
+#ifdef PFS_WAVE_TRACE
+  DevBuf<uint64_t> d_wtrace;    // development builds: per hash wave end time + hardware slot
+#endif
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned,
                                 // less d_counts[6] the settled cuts removed)
+  uint32_t scan_mode = 0;       // the last scan's PFSCDC_SCAN_SKIPPED_* bits
   uint64_t scanned_bytes = 0;   // bytes the last waited-for scan rolled (copied in pfscdc_wait)
   bool cuts_only = false;       // the last pfscdc_scan left the DataRef hashes to commit_refs
   DevBuf<uint64_t> d_entries, d_counts;  // d_counts: [0] n_entries
@@ -158,73 +161,29 @@ const pfscdc_params& ctx_params(const pfscdc_ctx* ctx) { return ctx->params; }
 
 namespace {
 
-// PFSCDC_HASH_BINS=0: no hash bins (every segment its own queue entry; A/B)
-bool hash_bins_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_HASH_BINS");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// PFSCDC_HASH_FAIR=0: hash bins without the fair-share issue priority; =2: fair share on LPT
-// launches without bins too (A/B)
-bool hash_fair_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_HASH_FAIR");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-bool hash_fair_forced() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_HASH_FAIR");
-    return e && atoi(e) == 2;
-  }();
-  return on;
-}
-
 // Scan workgroups: one per CU (each takes a whole CU's LDS), at most the tiles.  A workgroup
 // that finds no CU free waits for one, and the launch ends only after every workgroup has run:
 // with other streams' chain-bound hash launches resident on some CUs (c3's streams in flight,
-// which reserve their CUs), a full-width scan waits for them.  PFSCDC_SCAN_GRID=n caps the
-// workgroups (read per launch; the work queue spreads the units over however many run).
+// which reserve their CUs), a full-width scan waits for them.  The PFSCDC_SCAN_GRID knob caps
+// the workgroups (the work queue spreads the units over however many run).
 static int scan_grid(uint64_t ntiles, int num_cus) {
   uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)num_cus);
-  const char* e = getenv("PFSCDC_SCAN_GRID");
-  const int cap = e ? atoi(e) : 0;
+  const int64_t cap = knob(Knob::ScanGrid);
   if (cap > 0 && (uint64_t)cap < g) g = (uint64_t)cap;
   return (int)g;
 }
 
-// PFSCDC_HASH_CU_EXCLUSIVE=0: chain-bound scan hashes may share CUs with another launch (A/B)
-bool hash_cu_exclusive() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_HASH_CU_EXCLUSIVE");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// PFSCDC_SCAN_SKIP=0 scans every byte of a batch (A/B only: same results either way)
-bool scan_skip_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_SCAN_SKIP");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
+// Waves per SIMD of a hash launch (the PFSCDC_HASH_WAVES knob forces a count)
+static int knob_waves(uint64_t longest, uint64_t sum, int num_cus) {
+  return hash_waves(longest, sum, num_cus, (int)knob(Knob::HashWaves));
 }
 
 // The scan also skips the min - 1 positions after each file's cuts once they are settled
-// (ScanPlan).  Exact for min - 1 >= one work unit (pfscdc_internal.h).  PFSCDC_SCAN_CUTSKIP=0
-// turns it off, 2 / 3 keep the rank order with reports / without and never skip (A/B only:
-// same results either way); read per launch.  Returns the mode, 0 = off.
-uint32_t cut_skip_mode(const pfscdc_params& p) {
-  const char* e = getenv("PFSCDC_SCAN_CUTSKIP");
-  const int m = e && *e ? atoi(e) : 1;
-  if (m < 1 || m > 3) return 0;
-  const bool exact = (uint64_t)p.min_chunk >= kScanUnit + 1 && p.max_chunk > p.min_chunk;
-  return exact ? (uint32_t)m : 0u;
+// (ScanPlan).  Exact for min - 1 >= one work unit (pfscdc_internal.h); the PFSCDC_SCAN_CUTSKIP
+// knob turns it off.
+bool cut_skip_exact(const pfscdc_params& p) {
+  return knob(Knob::ScanCutSkip) != 0 && (uint64_t)p.min_chunk >= kScanUnit + 1 &&
+         p.max_chunk > p.min_chunk;
 }
 
 int fail(pfscdc_ctx* c, int code, const std::string& msg) {
@@ -484,14 +443,14 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
     longest_file = std::max(longest_file, len);
   }
   // the hash's longest chain is at most the largest file and at most max_chunk
-  const int waves = hash_waves(std::min<uint64_t>(longest_file, (uint64_t)p.max_chunk), nbytes,
-                               c->num_cus);
+  const int waves = knob_waves(std::min<uint64_t>(longest_file, (uint64_t)p.max_chunk), nbytes,
+                              c->num_cus);
   // hash bins: the files of at most one quad's share of the bytes are hashed whole by one
-  // quad each (lpt_order_block); PFSCDC_HASH_BINS=0: every segment its own queue entry (A/B)
+  // quad each (lpt_order_block); the PFSCDC_HASH_BIN_BYTES knob fixes the bin size (0: every
+  // segment its own queue entry)
   const uint64_t quads = (uint64_t)c->num_cus * 4 * (uint64_t)waves * 16;
-  uint64_t bin_bytes = hash_bins_enabled() ? (nbytes + quads - 1) / quads : 0;
-  if (const char* e = getenv("PFSCDC_HASH_BIN_BYTES"))  // a fixed bin size (tests, A/B)
-    bin_bytes = strtoull(e, nullptr, 10);
+  const int64_t kb = knob(Knob::HashBinBytes);
+  const uint64_t bin_bytes = kb >= 0 ? (uint64_t)kb : (nbytes + quads - 1) / quads;
   c->h_seg_base.p[nfiles] = cap;
   c->slot_cap = cap;
   c->nfiles = nfiles;
@@ -543,10 +502,13 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   HIP_OK(c, reset_spans(c, st));
 
   HIP_OK(c, hipEventRecord(c->ev[0], st));
+  c->scan_skipped = false;
+  c->scan_mode = 0;
   if (c->ntiles) {  // scan + (last workgroup) compaction into the sorted entry list
     // the first min - 1 bytes of every file hold no cut point: those strip steps are skipped
     const uint32_t* skip = nullptr;
-    c->scan_skipped = scan_skip_enabled();
+    c->scan_skipped = knob(Knob::ScanSkip) != 0;
+    c->scan_mode = c->scan_skipped ? PFSCDC_SCAN_SKIPPED_FIRST_MIN : 0u;
     const ScanPlan* d_plan = nullptr;
     const uint64_t nunits = c->ntiles * kScanWaves;
     if (c->scan_skipped) {
@@ -555,8 +517,8 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
       // nothing, keep the plain form)
       const bool cs_room = nfiles < kPlanMaxFiles &&
                            (uint64_t)nfiles * kRankSlots * sizeof(uint32_t) * 64 <= nbytes;
-      const uint32_t cs_mode = cs_room ? cut_skip_mode(p) : 0u;
-      if (cs_mode) {
+      if (cs_room && cut_skip_exact(p)) {
+        c->scan_mode |= PFSCDC_SCAN_SKIPPED_CUTS;
         // and past every cut the scan has settled (ScanPlan: rank order, per-file rank slots)
         HIP_OK(c, c->d_uinfo.ensure(2 * nunits));
         HIP_OK(c, c->d_uslots.ensure(nunits));
@@ -567,7 +529,7 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
         HIP_OK(c, c->d_planhdr.ensure(1));
         const ScanPlan hdr{c->d_uslots.p, c->d_plan.p, c->d_uinfo.p, c->d_rslots.p, c->d_offs.p,
                            (uint64_t)p.min_chunk, (uint64_t)p.max_chunk,
-                           (unsigned long long*)(c->d_counts.p + 6), cs_mode};
+                           (unsigned long long*)(c->d_counts.p + 6)};
         HIP_OK(c, launch_scan_plan(c->d_offs.p, nfiles, nbytes, (uint64_t)p.min_chunk, c->ntiles,
                                    c->d_skip.p, c->d_counts.p + 3, c->d_uinfo.p, c->d_uslots.p,
                                    c->d_plan.p, hdr, c->d_planhdr.p, st));
@@ -600,19 +562,26 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   // enqueued hash (the scans still overlap the hash tails; two hashes never share the CUs)
   if (c->hash_after && c->hash_after->device == c->device)
     HIP_OK(c, hipStreamWaitEvent(st, c->hash_after->ev[4], 0));
-  const char* wtrace = getenv("PFSCDC_WAVE_TRACE");
+#ifdef PFS_WAVE_TRACE
+  const char* wtrace = getenv("PFS_WAVE_TRACE_FILE");  // development builds only
   if (wtrace) {
     HIP_OK(c, c->d_wtrace.ensure(1 << 17));
     HIP_OK(c, hipMemsetAsync(c->d_wtrace.p, 0, sizeof(uint64_t) << 17, st));
     HIP_OK(c, set_wave_trace(c->d_wtrace.p, st));
   }
+#endif
+  // a chain-bound launch (one wave per SIMD) keeps its CUs to itself (launch_blake2b); with
+  // hash bins the waves of a SIMD share the issue fairly (the PFSCDC_HASH_FAIR knob)
   if (nfiles && !(options & kScanNoHash))
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, qlen, cap,
                              c->d_order.p, c->d_qctr.p, c->num_cus, nbytes, st, true,
-                             c->d_span.p + 2, waves, 0u, waves == 1 && hash_cu_exclusive(), next,
-                             hash_fair_enabled() && waves > 1 && (next || hash_fair_forced())
-                                 ? c->d_counts.p + 5 : nullptr));
+                             c->d_span.p + 2, waves, 0u, waves == 1, next,
+                             knob(Knob::HashFair) && waves > 1 && next ? c->d_counts.p + 5
+                                                                      : nullptr,
+                             (uint32_t)knob(Knob::HashFairEvery)));
+#ifdef PFS_WAVE_TRACE
   if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
+#endif
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
@@ -675,7 +644,8 @@ int pfscdc_wait(pfscdc_ctx* c) {
   c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] - c->h_span.p[kSpanSlots + 3] : c->nbytes;
   c->nsegs = total;
   c->scan_valid = true;
-  if (const char* wtrace = getenv("PFSCDC_WAVE_TRACE")) {  // development trace: append
+#ifdef PFS_WAVE_TRACE
+  if (const char* wtrace = getenv("PFS_WAVE_TRACE_FILE")) {  // development trace: append
     std::vector<uint64_t> t(1 << 17);
     HIP_OK(c, hipMemcpy(t.data(), c->d_wtrace.p, sizeof(uint64_t) << 17, hipMemcpyDeviceToHost));
     uint64_t sp[4];
@@ -686,6 +656,7 @@ int pfscdc_wait(pfscdc_ctx* c) {
       fclose(f);
     }
   }
+#endif
   return PFSCDC_OK;
 }
 
@@ -767,6 +738,13 @@ int pfscdc_last_scan_bytes(pfscdc_ctx* c, uint64_t* out) {
   return PFSCDC_OK;
 }
 
+int pfscdc_last_scan_mode(pfscdc_ctx* c, uint32_t* mode) {
+  if (!c || !mode) return PFSCDC_EINVAL;
+  if (c->pending) return fail(c, PFSCDC_ESTATE, "scan pending");
+  *mode = c->scan_mode;
+  return PFSCDC_OK;
+}
+
 int pfscdc_last_timings(pfscdc_ctx* c, float out[5]) {
   if (!c || !out) return PFSCDC_EINVAL;
   HIP_OK(c, hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]));
@@ -844,7 +822,7 @@ int pfscdc_get_chunks(pfscdc_ctx* c, const void* ctext, uint64_t nbytes, int cte
   for (uint32_t i = 0; i < nchunks; i++) longest = std::max(longest, c->h_segs.p[i].size);
   HIP_OK(c, launch_get(in, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, nchunks, c->d_order.p,
                        c->d_qctr.p, c->num_cus, nbytes, c->d_refs.p, outp, st,
-                       hash_waves(longest, nbytes, c->num_cus)));
+                       knob_waves(longest, nbytes, c->num_cus)));
   HIP_OK(c, hipEventRecord(c->ev[6], st));
   HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * nchunks,
                            hipMemcpyDeviceToHost, st));
@@ -900,56 +878,22 @@ int pfscdc_create_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
 // long set's launches always find room on every SIMD.  The two sets read and (in place)
 // write disjoint bytes.  Returns kOnePass when the chunk list does not allow it.
 constexpr int kOnePass = 1;
-constexpr uint32_t kNoPrio = 0x40000000u;  // hash launch prio_blocks: never raise priority
 
-// read at every call (tests switch them per call).  PFSCDC_COMMIT_TWO_SETS: 0 off, 1 on,
-// unset auto: on when the commit's chunks outnumber the quads of one wave per SIMD (the
-// chunk chains alone then keep the GPU busy past the longest chunk's two chains: c4 at two
-// commits per step, 28K chunks, 342 -> 362 GiB/s; at one commit, 14K chunks, the one-pass
-// form is faster: 248 vs 230-233 GiB/s, profiles/r3/two_sets/)
+// PFSCDC_COMMIT_TWO_SETS knob: 0 off, 1 on, -1 (default) auto: on when the commit's chunks
+// outnumber the quads of one wave per SIMD (the chunk chains alone then keep the GPU busy past
+// the longest chunk's two chains: c4 at two commits per step, 28K chunks, 342 -> 362 GiB/s; at
+// one commit, 14K chunks, the one-pass form is faster: 248 vs 230-233 GiB/s,
+// profiles/r3/two_sets/)
 static bool commit_two_sets(uint32_t nchunks, int num_cus) {
-  const char* e = getenv("PFSCDC_COMMIT_TWO_SETS");
-  if (e && *e) return atoi(e) != 0;
+  const int64_t k = knob(Knob::CommitTwoSets);
+  if (k >= 0) return k != 0;
   return (uint64_t)nchunks > (uint64_t)num_cus * 4 * 16;
 }
-// the long set: chunks longer than this percentage of the longest (PFSCDC_COMMIT_LONG_PCT;
-// c4 G = 2: 10% 335, 20% 305, 30% 362, 35% 356, 40% 338, 50% 305 GiB/s)
-static uint64_t commit_long_pct() {
-  const char* e = getenv("PFSCDC_COMMIT_LONG_PCT");
-  const int x = e ? atoi(e) : 0;
-  return (uint64_t)(x > 0 && x < 100 ? x : 30);
-}
-
-static bool commit_long_chains() {
-  const char* e = getenv("PFSCDC_COMMIT_LONG_CHAINS");
-  return e && atoi(e) != 0;
-}
-static int commit_long_waves() {  // PFSCDC_COMMIT_LONG_WAVES: the long set's (0: its own)
-  const char* e = getenv("PFSCDC_COMMIT_LONG_WAVES");
-  const int x = e ? atoi(e) : 0;
-  return x >= 1 && x <= 2 ? x : 0;
-}
-static int commit_long_create_waves() {  // PFSCDC_COMMIT_LONG_CREATE_WAVES (0: its own)
-  const char* e = getenv("PFSCDC_COMMIT_LONG_CREATE_WAVES");
-  const int x = e ? atoi(e) : 0;
-  return x >= 1 && x <= 2 ? x : 0;
-}
-// PFSCDC_COMMIT_LONG_PRIO (default 1): the long set's hash launches raise their issue priority
-// (s_setprio 2 while a quad has a block left); 0: no priority.  PFSCDC_COMMIT_CHACHA_PRIO
-// (default 1): the long set's ChaCha20 pass likewise.  A/B knobs.
-static bool commit_long_prio() {
-  const char* e = getenv("PFSCDC_COMMIT_LONG_PRIO");
-  return !(e && *e && atoi(e) == 0);
-}
-static bool commit_chacha_prio() {
-  const char* e = getenv("PFSCDC_COMMIT_CHACHA_PRIO");
-  return !(e && *e && atoi(e) == 0);
-}
-static int commit_short_waves() {  // PFSCDC_COMMIT_SHORT_WAVES: the short set's waves per SIMD
-  const char* e = getenv("PFSCDC_COMMIT_SHORT_WAVES");
-  const int x = e ? atoi(e) : 0;
-  return x >= 1 && x <= 2 ? x : 1;
-}
+// The long set: chunks longer than the PFSCDC_COMMIT_LONG_PCT knob's percentage of the longest
+// (c4 G = 2: 10% 335, 20% 305, 30% 362, 35% 356, 40% 338, 50% 305 GiB/s).  Its hash launches
+// and its ChaCha20 pass raise their issue priority; the short set runs at one wave per SIMD.
+// Measured and rejected (round 3-4, no longer built): the long set hashing only its chunks'
+// content chains (331 vs 362 GiB/s), other wave counts for either set, and no priority.
 
 static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
                                 const std::vector<uint64_t>& sbeg, const std::vector<uint64_t>& ssz,
@@ -976,7 +920,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     if (hash_known[i] && known_seg[i] < 0) return kOnePass;  // the one-pass form reports it
     longest = std::max(longest, co[i + 1] - co[i]);
   }
-  const uint64_t thr = longest * commit_long_pct() / 100;
+  const uint64_t thr = longest * (uint64_t)knob(Knob::CommitLongPct) / 100;
   std::vector<uint8_t> set_of(nchunks);  // 0: long, 1: short
   uint32_t nlong = 0;
   for (uint32_t i = 0; i < nchunks; i++) {
@@ -1015,18 +959,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
     sel[set_of[i]].push_back(i);
     if (!hash_known[i]) rec_chunk[set_of[i]].push_back(i);
   }
-  // chains only (PFSCDC_COMMIT_LONG_CHAINS=1, A/B): the long set hashes only its chunks'
-  // content chains (a one-segment chunk's is its segment); the segments inside its
-  // multi-DataRef chunks go to the short set, and the long set's in-place ChaCha20 waits for
-  // the short set's hashes (they read those bytes).  Slower: its unions end sooner (240 vs 296
-  // ms on c4 G = 2) but the long set's chunk.Create then waits for the short set's, which holds
-  // every segment at one wave per SIMD (331 vs 362 GiB/s, profiles/r3/two_sets/chains_*)
-  const bool chains_only = commit_long_chains();
-  for (uint64_t s = 0; s < m; s++) {
-    const uint32_t i = seg_chunk[s];
-    const bool own = set_of[i] == 0 && (!chains_only || hash_known[i]);
-    rec_seg[own ? 0 : 1].push_back(s);
-  }
+  for (uint64_t s = 0; s < m; s++) rec_seg[set_of[seg_chunk[s]]].push_back(s);
   HIP_OK(c, hipEventRecord(c->pev[0], c->stream));  // the scan and the bytes are ready
   HIP_OK(c, hipStreamWaitEvent(X[1]->stream, c->pev[0], 0));
   for (int x = 0; x < 2; x++) {
@@ -1066,13 +999,11 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
                                hipMemcpyHostToDevice, st));
     HIP_OK(c, hipMemcpyAsync(u->d_counts.p + 1, u->h_seg_begin.p, sizeof(uint64_t),
                              hipMemcpyHostToDevice, st));
-    const int w = hash_waves(lg, sum, u->num_cus);
+    const int w = knob_waves(lg, sum, u->num_cus);
     if (R)
       HIP_OK(c, launch_blake2b(data, u->d_offs.p, u->d_segs.p, u->d_counts.p + 1, R, u->d_order.p,
                                u->d_qctr.p, u->num_cus, nbytes, st, false, nullptr,
-                               x ? std::min(w, commit_short_waves())
-                                 : chains_only ? 1 : commit_long_waves() ? commit_long_waves() : w,
-                               x || !commit_long_prio() ? kNoPrio : 1u));
+                               x ? std::min(w, 1) : w, x ? kHashPrioNone : 1u));
     if (R)
       HIP_OK(c, hipMemcpyAsync(u->h_segs.p, u->d_segs.p, sizeof(pfscdc_segment) * R,
                                hipMemcpyDeviceToHost, st));
@@ -1097,11 +1028,10 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
       for (uint32_t i : sel[x])
         if (hash_known[i])
           std::memcpy(content_hashes + 32ull * i, segment_hashes + 32 * known_seg[i], 32);
-      u->cr_wave_cap = x ? commit_short_waves() : commit_long_create_waves();
-      u->cr_hash_prio = x || !commit_long_prio() ? kNoPrio : 1u;
-      u->cr_chacha_prio = x == 0 && commit_chacha_prio();
+      u->cr_wave_cap = x ? 1 : 0;
+      u->cr_hash_prio = x ? kHashPrioNone : 1u;
+      u->cr_chacha_prio = x == 0;
       u->cr_one_stream = true;  // each set has one stream (two in all)
-      if (x == 0 && chains_only) HIP_OK(c, hipStreamWaitEvent(c->stream, c->pev[2], 0));
       const int rc = create_refs_device(u, data, nbytes, co, nchunks, content_hashes, all.data(),
                                         refs, ct, sel[x].data(), (uint32_t)sel[x].size(), false);
       u->cr_wave_cap = 0;
@@ -1129,7 +1059,7 @@ static int commit_refs_two_sets(pfscdc_ctx* c, const uint8_t* data, uint64_t nby
   for (int x = 0; x < 2; x++)
     if (hipEventElapsedTime(&ms, c->pev[0], X[x]->ev[6]) == hipSuccess) b = std::max(b, ms);
   drain.armed = false;  // create_refs_finish waited for both streams
-  if (getenv("PFSCDC_TRACE")) {  // each set's timeline (ms after the scan): hashes, chunk.Create
+  if (knob(Knob::Trace)) {  // each set's timeline (ms after the scan): hashes, chunk.Create
     float t[4] = {0, 0, 0, 0};
     for (int x = 0; x < 2; x++) {
       (void)hipEventElapsedTime(&t[x], c->pev[0], c->pev[1 + x]);
@@ -1244,7 +1174,7 @@ int pfscdc_commit_refs(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int by
   if (R)
     HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, R, c->d_order.p,
                              c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
-                             hash_waves(longest, sum, c->num_cus)));
+                             knob_waves(longest, sum, c->num_cus)));
   HIP_OK(c, hipEventRecord(e1, st));
   if (R)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * R,
@@ -1583,7 +1513,7 @@ int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
   }
   HIP_OK(c, launch_blake2b(data, c->d_offs.p, c->d_segs.p, c->d_counts.p + 1, n, c->d_order.p,
                            c->d_qctr.p, c->num_cus, nbytes, st, false, nullptr,
-                           hash_waves(longest, sum, c->num_cus)));
+                           knob_waves(longest, sum, c->num_cus)));
   HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, sizeof(pfscdc_segment) * n,
                            hipMemcpyDeviceToHost, st));
   HIP_OK(c, hipStreamSynchronize(st));
@@ -1594,33 +1524,17 @@ int hash_records_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes,
 }
 
 // Split Ref.Id pass (ChaCha20 in parallel, then BLAKE2b of the ciphertext) when the chunk list
-// cannot fill the hash grid's quads, i.e. the pass is bound by its longest chains.
-// PFSCDC_REFID_SPLIT=0/1 forces either form (A/B and tests).
-static bool refid_twostream() {
-  static const bool on = [] {
-    const char* e = getenv("PFSCDC_REFID_TWOSTREAM");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// the long subset of a two-stream Ref.Id pass: chunks longer than this percentage of the
-// longest (PFSCDC_REFID_LONG_PCT, A/B; default 65)
-static uint64_t refid_long_pct() {
-  static const uint64_t v = [] {
-    const char* e = getenv("PFSCDC_REFID_LONG_PCT");
-    const int x = e ? atoi(e) : 0;
-    return (uint64_t)(x > 0 && x < 100 ? x : 65);
-  }();
-  return v;
-}
-
+// cannot fill the hash grid's quads, i.e. the pass is bound by its longest chains.  The
+// PFSCDC_REFID_SPLIT knob forces either form (0 fused, 1 split).
 static bool refid_split(uint32_t n, int num_cus) {
-  const char* e = getenv("PFSCDC_REFID_SPLIT");
-  if (e && *e) return atoi(e) != 0;
+  const int64_t k = knob(Knob::RefIdSplit);
+  if (k >= 0) return k != 0;
   const uint64_t quads = (uint64_t)num_cus * 4 * kHashWavesPerSimd * 16;
   return n <= quads;
 }
+
+// the long subset of a two-stream Ref.Id pass: chunks longer than 65% of the longest
+constexpr uint64_t kRefIdLongPct = 65;
 
 // chunk.Create(ctx, CreateOptions{}, chunk, createFunc) for n chunks of a device buffer
 // (transform.go:26-46): dek = Hash(Hash(chunk)) (deriveKey :173-178), id = Hash(ChaCha20_dek
@@ -1652,24 +1566,24 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   // two contexts: one wave per SIMD and no priority for the short set, so the long set's
   // launches always find room and issue first)
   auto waves_for = [&](uint64_t longest, uint64_t sum) {
-    const int w = hash_waves(longest, sum, c->num_cus);
+    const int w = knob_waves(longest, sum, c->num_cus);
     return c->cr_wave_cap > 0 && w > c->cr_wave_cap ? c->cr_wave_cap : w;
   };
   // With every content hash known (pfscdc_commit_refs), a split Ref.Id pass runs on two
   // streams: the chunks longer than half the longest first on the ctx stream (their ChaCha20
   // pass is short, so the serial BLAKE2b chains that bound the pass start right away), the
   // rest on a second stream beside them (its ChaCha20 pass and shorter chains fit in the long
-  // chains' shadow).  PFSCDC_REFID_TWOSTREAM=0: one stream (A/B).
+  // chains' shadow).
   // The split point: the long set is the chunks longer than 65% of the longest
-  // (PFSCDC_REFID_LONG_PCT, A/B).  c4 commit, Ref.Id pass: 50% 230, 65% 208-211, 80% 227,
+  // (kRefIdLongPct).  c4 commit, Ref.Id pass: 50% 230, 65% 208-211, 80% 227,
   // 90% 246 ms, one stream 240 ms: a larger long set lengthens its own ChaCha20 pass, a
   // smaller one leaves rest chains that outlast the longest one (they run at two waves per
   // SIMD, slower than a lone chain).
   uint32_t nl = 0;
-  if (k == 0 && nr > 1 && refid_twostream() && !c->cr_one_stream) {
+  if (k == 0 && nr > 1 && !c->cr_one_stream) {
     uint64_t longest = 0;
     for (uint32_t t = 0; t < nr; t++) longest = std::max(longest, size_of(chunk_of(t)));
-    const uint64_t thr = longest * refid_long_pct() / 100;
+    const uint64_t thr = longest * kRefIdLongPct / 100;
     auto is_long = [&](uint32_t i) { return size_of(i) > thr; };
     std::stable_partition(c->perm.begin(), c->perm.end(), is_long);
     for (uint32_t t = 0; t < nr; t++) nl += is_long(chunk_of(t)) ? 1 : 0;
@@ -1728,7 +1642,7 @@ int create_refs_device(pfscdc_ctx* c, const uint8_t* data, uint64_t nbytes, cons
   uint8_t* ct = ctext_out;
   // the ciphertext over the plaintext (PFSCDC_OPT_CTEXT_IN_PLACE) always takes the split form:
   // the fused kernel reads its plaintext and writes its ciphertext through two __restrict__
-  // pointers, which must not alias (PFSCDC_REFID_SPLIT=0 cannot force it here)
+  // pointers, which must not alias (the PFSCDC_REFID_SPLIT knob cannot force it here)
   const bool in_place = ct != nullptr && ct == data;
   bool split = in_place || refid_split(nr, c->num_cus);
   if (split && !ct) {

@@ -51,6 +51,17 @@ static_assert(sizeof(TileRec) == 64, "tile record is one 64-byte line");
 static_assert(sizeof(pfscdc_segment) == 56, "segment record layout");
 static_assert(sizeof(pfscdc_ref) == 64, "ref record layout");
 
+// Tuning knobs (knobs.cpp): process-wide integers, read from the environment once.
+enum class Knob : int {
+  ScanSkip, ScanCutSkip, ScanGrid,
+  HashBinBytes, HashWaves, HashFair, HashFairEvery,
+  RefIdSplit, CommitTwoSets, CommitLongPct,
+  UwWorkers, UwInflight, UwMirror, UwIndexGrouped, UwArenaPoolBytes, CtxCache, CopyThreads,
+  Trace,
+  kCount
+};
+int64_t knob(Knob k);
+
 void generate_hashes(int64_t seed, uint64_t out[256]);
 const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
 void go_int63(int64_t seed, int64_t* out, int n);
@@ -98,7 +109,9 @@ bool ctx_scan_valid(const pfscdc_ctx* ctx);
 uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
 uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
-hipError_t set_wave_trace(uint64_t* p, hipStream_t st);  // development trace (PFSCDC_WAVE_TRACE)
+#ifdef PFS_WAVE_TRACE
+hipError_t set_wave_trace(uint64_t* p, hipStream_t st);  // development builds: per-wave trace
+#endif
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 
 // Scan work unit = one wave's 64 strips of a tile; kUnitSteps 128-byte strip steps of
@@ -127,7 +140,6 @@ struct ScanPlan {
   const uint64_t* offs;   // file offsets (nfiles + 1)
   uint64_t min_chunk, max_chunk;
   unsigned long long* dyn_skipped;  // bytes the settled cuts removed from the scan
-  uint32_t mode;  // 1: skip past settled cuts; A/B only: 2 rank order + reports, 3 rank order
 };
 hipError_t launch_scan(const uint8_t* data, const uint8_t* tail, uint64_t n, const uint64_t* d_table,
                        uint32_t average_bits, uint64_t ntiles, TileRec* recs, int grid,
@@ -158,16 +170,23 @@ hipError_t launch_select(const uint8_t* data, const uint64_t* d_table, const uin
 hipError_t launch_segcompact(const pfscdc_segment* slots, const uint64_t* seg_base,
                              const uint64_t* nseg, uint32_t nfiles, pfscdc_segment* segs,
                              uint64_t* seg_begin, hipStream_t st);
+// Hash issue priority (launcher argument prio): 0 = the default (kHashPrioAuto: raise it for
+// chains of more than 8192 blocks when quads refill), kHashPrioNone = never, else a threshold
+// in 128-B blocks.
+constexpr uint32_t kHashPrioAuto = 0x3fffffffu;
+constexpr uint32_t kHashPrioNone = 0x80000000u;
 hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,
                           const uint64_t* seg_count, uint64_t max_segments, uint32_t* order,
                           uint32_t* counter, int num_cus, uint64_t nbytes, hipStream_t st,
                           bool ordered = false, uint64_t* span = nullptr, int waves = 0,
-                          uint32_t prio = 0,  // prio: issue-priority threshold (0: default)
+                          uint32_t prio = 0,  // issue priority (see kHashPrioNone)
                           bool cu_exclusive = false,  // one workgroup per CU (see launcher)
                           const uint32_t* next = nullptr,  // hash bins (lpt_order_block)
-                          uint64_t* fair = nullptr);  // bins: fair-share counter (zeroed)
-// waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all
-int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus);
+                          uint64_t* fair = nullptr,  // bins: fair-share counter (zeroed)
+                          uint32_t fair_every = 256);  // blocks between fair-share updates
+// waves per SIMD for a hash launch over chains of at most longest_bytes, total_bytes in all;
+// forced in 1..8 (the PFSCDC_HASH_WAVES knob) overrides
+int hash_waves(uint64_t longest_bytes, uint64_t total_bytes, int num_cus, int forced);
 hipError_t launch_order(const pfscdc_segment* segs, const uint64_t* seg_count, uint32_t* order,
                         uint32_t* counter, hipStream_t st);
 hipError_t launch_ref_ids(const uint8_t* data, const uint64_t* offs, pfscdc_segment* segs,

@@ -628,7 +628,7 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n, double* stage_ms,
     }
     return PFSCDC_OK;
   }
-  const bool trace = getenv("PFSCDC_TRACE") != nullptr;
+  const bool trace = knob(Knob::Trace) != 0;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   const auto t0 = now();

@@ -19,3 +19,22 @@ def gpu_available():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return True
+
+
+@pytest.fixture
+def knob():
+    """Set library tuning knobs (pfscdc_set_knob) for one test; restored afterwards.
+    knob("PFSCDC_SCAN_GRID", 1); a value of None restores the knob's default."""
+    from pfs_amd import _lib
+
+    old = {}
+    info = _lib.knob_info()
+
+    def set_(name, value):
+        if name not in old:
+            old[name] = _lib.get_knob(name)
+        _lib.set_knob(name, info[name][2] if value is None else int(value))
+
+    yield set_
+    for k, v in old.items():
+        _lib.set_knob(k, v)

@@ -5,6 +5,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -73,6 +74,92 @@ def test_ctx_create_rejects_bad_params(lib):
     assert lib.pfscdc_ctx_create(C.byref(p), 0, C.byref(ctx)) == _lib.PFSCDC_EUNSUPPORTED
     p = _lib.Params(23, 0, 1, 5000, 1000)  # max < min
     assert lib.pfscdc_ctx_create(C.byref(p), 0, C.byref(ctx)) == _lib.PFSCDC_EINVAL
+
+
+INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
+
+
+def documented_knobs():
+    """The first column of INTEGRATION.md's knob table: name -> (default, lo, hi)."""
+    text = open(INTEGRATION).read()
+    table = text.split("<!-- knob list:", 1)[1]
+    out = {}
+    for m in re.finditer(r"^\| `(PFSCDC_[A-Z0-9_]+)` \| (-?\d+) \| (-?\d+)–(\S+) \|", table, re.M):
+        hi = m.group(4)
+        hi = 1 << int(hi[2:]) if hi.startswith("2^") else int(hi)
+        out[m.group(1)] = (int(m.group(2)), int(m.group(3)), hi)
+    return out
+
+
+def header_macros():
+    return set(re.findall(r"#define\s+(PFSCDC_[A-Z0-9_]+)", open(HEADER).read()))
+
+
+def test_knob_table_equals_integration_list(lib):
+    """The knobs the library has are exactly the documented ones, with their defaults and
+    ranges (no undocumented A/B branch a stray variable could select)."""
+    doc = documented_knobs()
+    lib_knobs = _lib.knob_info()
+    assert set(lib_knobs) == set(doc)
+    for name, (lo, hi, d) in lib_knobs.items():
+        assert doc[name] == (d, lo, hi), name
+
+
+def test_library_strings_name_only_documented_knobs(lib):
+    """Every PFSCDC_* string inside libpfscdc.so (what a getenv could name) is a documented
+    knob or a macro of the public header (option names in error messages)."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    found = {m.decode() for m in re.findall(rb"PFSCDC_[A-Z0-9_]+", blob)}
+    allowed = set(documented_knobs()) | header_macros()
+    assert found - allowed == set(), sorted(found - allowed)
+    assert set(documented_knobs()) <= found
+
+
+def test_sources_read_the_environment_only_in_knobs_cpp():
+    """getenv appears only in knobs.cpp, or inside the development-build wave trace
+    (#ifdef PFS_WAVE_TRACE, not compiled into the product library)."""
+    csrc = os.path.join(ROOT, "pfs_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f == "knobs.cpp" or not f.endswith((".cpp", ".hip", ".h")):
+            continue
+        depth = 0  # nesting of #ifdef PFS_WAVE_TRACE
+        stack = []
+        for ln, line in enumerate(open(os.path.join(csrc, f)), 1):
+            s = line.strip()
+            if s.startswith("#if"):
+                stack.append("PFS_WAVE_TRACE" in s)
+                depth += stack[-1]
+            elif s.startswith("#endif") and stack:
+                depth -= stack.pop()
+            code = line.split("//", 1)[0]
+            if "getenv" in code:
+                assert depth > 0, f"{f}:{ln} reads the environment outside knobs.cpp"
+
+
+def test_knob_set_get_and_ranges(lib):
+    d = _lib.get_knob("PFSCDC_SCAN_GRID")
+    with _lib.knobs(PFSCDC_SCAN_GRID=7):
+        assert _lib.get_knob("PFSCDC_SCAN_GRID") == 7
+    assert _lib.get_knob("PFSCDC_SCAN_GRID") == d
+    assert lib.pfscdc_set_knob(b"PFSCDC_HASH_WAVES", 9) == _lib.PFSCDC_EINVAL  # above 8
+    assert lib.pfscdc_set_knob(b"PFSCDC_SCAN_PAIR", 1) == _lib.PFSCDC_EINVAL  # removed form
+    v = C.c_int64()
+    assert lib.pfscdc_get_knob(b"PFSCDC_NOPE", C.byref(v)) == _lib.PFSCDC_EINVAL
+    assert lib.pfscdc_knob_info(-1, None, None, None) is None
+
+
+def test_environment_is_read_once_with_bad_values_ignored(tmp_path):
+    """A fresh process: a good variable sets its knob, a bad one keeps the default (and says
+    so on stderr), a removed A/B variable is ignored."""
+    code = ("from pfs_amd import _lib; import sys; "
+            "print(_lib.get_knob('PFSCDC_SCAN_GRID'), _lib.get_knob('PFSCDC_HASH_WAVES'), "
+            "_lib.get_knob('PFSCDC_COMMIT_LONG_PCT'))")
+    env = dict(os.environ, PFSCDC_SCAN_GRID="64", PFSCDC_HASH_WAVES="x", PFSCDC_COMMIT_LONG_PCT="100",
+               PFSCDC_SCAN_PAIR="1", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT,
+                       check=True)
+    assert r.stdout.split() == ["64", "0", "30"]
+    assert "PFSCDC_HASH_WAVES=x" in r.stderr and "PFSCDC_COMMIT_LONG_PCT=100" in r.stderr
 
 
 def test_product_does_not_import_oracle():

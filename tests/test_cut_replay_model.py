@@ -45,21 +45,26 @@ def select_cuts(cands, fs, fe, mn, mx):
 def plan_units(offs, mn):
     """scan_skip_kernel: per unit its static skip (steps), tracked file and rank."""
     n = int(offs[-1])
+    nfiles = len(offs) - 1
+    kall = U // STEP
     units = []
     for u in range((n + U - 1) // U):
         ub, ue = u * U, min((u + 1) * U, n)
         f = int(np.searchsorted(offs, ub, side="right") - 1)
-        s, tf, rank = U // STEP, None, 0
-        for g in range(f, min(f + 64, len(offs) - 1)):
-            if offs[g] >= ue:
+        s, tf, rank = 0, None, 0  # the kernel starts from "scan whole" (a crowded unit)
+        for g in range(f, f + 64):
+            if g >= nfiles or offs[g] >= ue:
+                s = kall
                 break
             ls, fe = int(offs[g]) + mn - 1, int(offs[g + 1])
             if ls < fe:
                 first = max(ls, ub)
-                s = (first - ub) // STEP if first < ue else U // STEP
+                s = (first - ub) // STEP if first < ue else kall
                 tf, rank = g, ub // U - ls // U
                 break
-        if s < U // STEP and ub + s * STEP < ue:
+        if tf is None:
+            s = kall  # plan mode: a crowded unit holds no eligible position, takes no slot
+        if s < kall and ub + s * STEP < ue:
             units.append((u, tf, rank, s))
     units.sort(key=lambda t: (min(t[2], 63), t[0]))
     return units
@@ -150,6 +155,29 @@ def test_replay_never_hides_a_cut(avg, mn, mx):
             for f in range(nfiles):
                 assert select_cuts(got, int(offs[f]), int(offs[f + 1]), mn, mx) == want[f], \
                     (trial, waves, stale, f)
+
+
+def test_crowded_units_take_no_slot_and_hide_no_cut():
+    """Units crowded with more than 64 sub-min files: with min - 1 >= one unit
+    they hold no eligible position, so they take no dispatch slot (the kernel's slot count and
+    the slots it fills must agree), and the cuts of the long files around them are unchanged."""
+    rng = np.random.default_rng(11)
+    mn, mx = 1100, 4000
+    lens = np.concatenate([[30 * U], np.full(400, 9), [25 * U], np.full(200, 13), [40 * U]])
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    units = plan_units(offs, mn)
+    assert all(tf is not None for (_, tf, _, _) in units)
+    crowded = [u for u in range(int(offs[-1]) // U)
+               if np.count_nonzero((offs[:-1] >= u * U) & (offs[:-1] < (u + 1) * U)) > 64]
+    assert crowded, "the layout must crowd at least one unit"
+    n = int(offs[-1])
+    cands = np.unique(rng.integers(0, n, n // 300))
+    want = [select_cuts(cands, int(offs[f]), int(offs[f + 1]), mn, mx)
+            for f in range(len(offs) - 1)]
+    for waves, stale in ((1, 0.0), (12, 0.5)):
+        got, nfiles = simulate(offs, cands, mn, mx, rng, waves, stale)
+        for f in range(nfiles):
+            assert select_cuts(got, int(offs[f]), int(offs[f + 1]), mn, mx) == want[f]
 
 
 def test_replay_skips_something_when_ranks_finish_in_order():

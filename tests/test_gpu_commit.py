@@ -166,9 +166,8 @@ def test_ciphertext_in_place_needs_device_bytes():
     c.close()
 
 
-@pytest.mark.parametrize("chains_only", ["0", "1"])
 @pytest.mark.parametrize("in_place", [False, True])
-def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkeypatch):
+def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, knob):
     """The two-set commit (the long chunks' hashes and chunk.Create on the ctx stream at issue
     priority, the rest on a helper context beside them, PFSCDC_COMMIT_TWO_SETS) gives the same
     DataRef hashes, content hashes, Refs and ciphertext as the one-pass form, at several
@@ -186,11 +185,9 @@ def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkey
     streams = [0, nf // 4, nf // 2, nf]
     cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
 
-    monkeypatch.setenv("PFSCDC_COMMIT_LONG_CHAINS", chains_only)
-
     def run(two_sets, pct):
-        monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "1" if two_sets else "0")
-        monkeypatch.setenv("PFSCDC_COMMIT_LONG_PCT", str(pct))
+        knob("PFSCDC_COMMIT_TWO_SETS", 1 if two_sets else 0)
+        knob("PFSCDC_COMMIT_LONG_PCT", pct)
         c = Chunker(cp, 0)
         c.set_cuts_only(True)
         c.set_ctext_in_place(in_place)
@@ -217,11 +214,10 @@ def test_commit_refs_two_chunk_sets_equal_one_pass(in_place, chains_only, monkey
         assert bytes(refs0[i]["id"]) == rid and bytes(refs0[i]["dek"]) == dek
 
 
-@pytest.mark.parametrize("chacha_coalesced", ["1", "0"])
-@pytest.mark.parametrize("refid_split", ["0", "1"])
-def test_ciphertext_in_place_whatever_the_refid_form(refid_split, chacha_coalesced, monkeypatch):
+@pytest.mark.parametrize("refid_split", [0, 1])
+def test_ciphertext_in_place_whatever_the_refid_form(refid_split, knob):
     """In place, chunk.Create always takes the split Ref.Id form: the fused kernel's plaintext
-    and ciphertext pointers are __restrict__ and must not alias, so PFSCDC_REFID_SPLIT=0 (or a
+    and ciphertext pointers are __restrict__ and must not alias, so the PFSCDC_REFID_SPLIT knob at 0 (or a
     chunk count above the quads, which picks the fused form) must not reach it with
     ctext_out == data.  Refs and the buffer equal the copy form's."""
     import torch
@@ -233,14 +229,10 @@ def test_ciphertext_in_place_whatever_the_refid_form(refid_split, chacha_coalesc
     host = synthetic_bytes(offs, 23)
     streams = [0, len(lens) // 2, len(lens)]
     cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
-    monkeypatch.setenv("PFSCDC_COMMIT_TWO_SETS", "0")
-    monkeypatch.setenv("PFSCDC_CHACHA_COALESCED", chacha_coalesced)
+    knob("PFSCDC_COMMIT_TWO_SETS", 0)
 
-    def run(in_place, split_env):
-        if split_env is None:
-            monkeypatch.delenv("PFSCDC_REFID_SPLIT", raising=False)
-        else:
-            monkeypatch.setenv("PFSCDC_REFID_SPLIT", split_env)
+    def run(in_place, split):
+        knob("PFSCDC_REFID_SPLIT", split)
         c = Chunker(cp, 0)
         c.set_cuts_only(True)
         c.set_ctext_in_place(in_place)
@@ -251,7 +243,7 @@ def test_ciphertext_in_place_whatever_the_refid_form(refid_split, chacha_coalesc
         c.close()
         return coffs, refs, chash, seg, t.cpu().numpy()
 
-    coffs, refs0, chash0, seg0, _ = run(False, None)
+    coffs, refs0, chash0, seg0, _ = run(False, -1)
     _, refs, chash, seg, ct = run(True, refid_split)
     assert np.array_equal(refs["id"], refs0["id"]) and np.array_equal(refs["dek"], refs0["dek"])
     assert np.array_equal(chash, chash0) and np.array_equal(seg, seg0)

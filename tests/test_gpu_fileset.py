@@ -90,14 +90,14 @@ def workload(seed, nfiles, max_len, dirs=4):
 
 @pytest.mark.parametrize("index_grouped", ["1", "0"])
 @pytest.mark.parametrize("inflight", [None, "300000"])
-def test_unordered_writer_many_filesets_multilevel_index(inflight, index_grouped, monkeypatch):
+def test_unordered_writer_many_filesets_multilevel_index(inflight, index_grouped, knob):
     # inflight: serialized filesets are written in groups of up to this many bytes (the
     # default holds all of them until Close); the output must not depend on the grouping.
     # index_grouped: a group's index writers closed level by level in grouped closes (the
     # default) or one fileset at a time
-    monkeypatch.setenv("PFSCDC_UW_INDEX_GROUPED", index_grouped)
+    knob("PFSCDC_UW_INDEX_GROUPED", index_grouped)
     if inflight:
-        monkeypatch.setenv("PFSCDC_UW_INFLIGHT", inflight)
+        knob("PFSCDC_UW_INFLIGHT", inflight)
     ops, _ = workload(1, 160, 40_000)
     ops.append(("delete", "/d1/", ""))
     ops.append(("put", "/d1/again", "", False, b"xyz" * 1000))
@@ -149,14 +149,14 @@ def test_reference_index_params_many_small_files_multilevel():
 
 
 @pytest.mark.parametrize("workers,mirror", [("2", "1"), ("3", "0"), ("1", "0")])
-def test_group_writers_and_upload_paths(workers, mirror, monkeypatch):
+def test_group_writers_and_upload_paths(workers, mirror, knob):
     """Round-3 write path: several groups in flight on group writers of their own ctxs
     (PFSCDC_UW_WORKERS), Put bytes uploaded into arena device mirrors as they arrive or
     uploaded at group time (PFSCDC_UW_MIRROR), the union hash launch per grouped close: the
     output must equal the restated reference whatever the grouping and upload path."""
-    monkeypatch.setenv("PFSCDC_UW_INFLIGHT", "300000")
-    monkeypatch.setenv("PFSCDC_UW_WORKERS", workers)
-    monkeypatch.setenv("PFSCDC_UW_MIRROR", mirror)
+    knob("PFSCDC_UW_INFLIGHT", 300000)
+    knob("PFSCDC_UW_WORKERS", workers)
+    knob("PFSCDC_UW_MIRROR", mirror)
     ops, _ = workload(3, 160, 40_000)
     want, got, wlog, glog = run_both(ops, SMALL, 400_000, SMALL_INDEX)
     assert len(want) >= 5
@@ -164,11 +164,11 @@ def test_group_writers_and_upload_paths(workers, mirror, monkeypatch):
 
 
 @pytest.mark.parametrize("workers", ["1", "2"])
-def test_large_puts_copy_pool_reference_params(workers, monkeypatch):
+def test_large_puts_copy_pool_reference_params(workers, knob):
     """Puts above the copy pool's 4 MiB split (the persistent copy threads) and files split
     across filesets, at the reference's chunking; one and two group writers."""
-    monkeypatch.setenv("PFSCDC_UW_WORKERS", workers)
-    monkeypatch.setenv("PFSCDC_UW_INFLIGHT", "15000000")
+    knob("PFSCDC_UW_WORKERS", workers)
+    knob("PFSCDC_UW_INFLIGHT", 15000000)
     data = synthetic_bytes([0, 40 << 20], 11).tobytes()
     ops = [("put", f"/f{i}", "", False, data[i * (9 << 20):(i + 1) * (9 << 20)]) for i in range(4)]
     ops.append(("put", "/g", "", False, data[36 << 20:]))

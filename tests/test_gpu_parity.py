@@ -236,7 +236,7 @@ def test_scan_skips_first_min_bytes_of_each_file(bits, min_):
         assert scanned < int(offs[-1]), "nothing skipped"
 
 
-def test_scan_skip_c2_layout_rolls_three_quarters(monkeypatch):
+def test_scan_skip_c2_layout_rolls_three_quarters(knob):
     # configs[1]: 4 MiB files, min 1,000,000: the first 999,999 bytes of each file hold no
     # eligible position, 23.8% of the bytes are never rolled (whole 8 KiB steps).  The
     # skipping past settled cuts is off here (it depends on timing); with it on, at most these
@@ -246,21 +246,28 @@ def test_scan_skip_c2_layout_rolls_three_quarters(monkeypatch):
     data = synthetic_bytes(offs, 0xC2)
     c = chunker_for(p)
     per_file = (4 << 20) - (999_999 // 8192) * 8192
-    monkeypatch.setenv("PFSCDC_SCAN_CUTSKIP", "0")
+    knob("PFSCDC_SCAN_CUTSKIP", 0)
     assert_same(c.scan(data, offs), data, offs, p)
     assert c.last_scan_bytes() == 8 * per_file
-    monkeypatch.delenv("PFSCDC_SCAN_CUTSKIP")
+    assert c.last_scan_mode() == _lib.SCAN_SKIPPED_FIRST_MIN
+    knob("PFSCDC_SCAN_CUTSKIP", None)
     assert_same(c.scan(data, offs), data, offs, p)
     assert 0 < c.last_scan_bytes() <= 8 * per_file
+    assert c.last_scan_mode() == _lib.SCAN_SKIPPED_FIRST_MIN | _lib.SCAN_SKIPPED_CUTS
+    knob("PFSCDC_SCAN_SKIP", 0)
+    assert_same(c.scan(data, offs), data, offs, p)
+    assert c.last_scan_bytes() == int(offs[-1]) and c.last_scan_mode() == 0
 
 
 def _cut_skip_layout(min_):
     """File lengths around min, the 256 KiB unit and the 8 KiB step, files with several cuts,
-    a constant-byte file, empty files."""
+    a constant-byte file, empty files, and whole units crowded with more than 64 sub-min
+    files between long files (such a unit must take no dispatch slot)."""
     U = 262_144
     lens = [0, 1, min_ - 1, min_, min_ + 1, U - 1, U, U + 1, 2 * min_, 2 * min_ + 8191,
             3 * min_ + U + 5, 0, 5 << 20, (2 << 20) + 77, 9 * min_ + 3, 1 << 20]
     lens += [(2 << 20) + 4096 * k for k in range(40)]
+    lens += [700] * 1200 + [(3 << 20) + 11] + [0, 300] * 400 + [4 * min_ + 9]
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     return lens, offs
 
@@ -268,7 +275,7 @@ def _cut_skip_layout(min_):
 @pytest.mark.parametrize("grid", ["1", "3", ""])
 @pytest.mark.parametrize("bits,min_,max_", [(16, 300_000, 1_200_000), (18, 262_145, 700_000),
                                             (17, 400_000, 4_000_000), (23, 300_000, 1_200_000)])
-def test_scan_skips_past_settled_first_cuts(monkeypatch, grid, bits, min_, max_):
+def test_scan_skips_past_settled_first_cuts(knob, grid, bits, min_, max_):
     """The scan takes its units in rank order and a unit whose file's first cut is settled
     skips the strip steps below cut + min (writer.go:167-170 after the reset at the cut).
     Candidates every 2^bits bytes put first cuts right after min; at 2^23 most first cuts
@@ -277,7 +284,7 @@ def test_scan_skips_past_settled_first_cuts(monkeypatch, grid, bits, min_, max_)
     earlier ranks have finished when the later ones start, so skipping happens; the full grid
     runs everything at once.  Results must equal the oracle's either way."""
     if grid:
-        monkeypatch.setenv("PFSCDC_SCAN_GRID", grid)
+        knob("PFSCDC_SCAN_GRID", grid)
     p = Ch.Params(average_bits=bits, seed=1, min=min_, max=max_)
     lens, offs = _cut_skip_layout(min_)
     data = synthetic_bytes(offs, 300 + bits)
@@ -286,10 +293,10 @@ def test_scan_skips_past_settled_first_cuts(monkeypatch, grid, bits, min_, max_)
     c = chunker_for(p)
     res = c.scan(data, offs)
     assert_same(res, data, offs, p)
-    monkeypatch.setenv("PFSCDC_SCAN_CUTSKIP", "0")
+    knob("PFSCDC_SCAN_CUTSKIP", 0)
     c.scan(data, offs)
     static = c.last_scan_bytes()
-    monkeypatch.delenv("PFSCDC_SCAN_CUTSKIP")
+    knob("PFSCDC_SCAN_CUTSKIP", None)
     c.scan(data, offs)
     rolled = c.last_scan_bytes()
     assert 0 < rolled <= static
@@ -325,21 +332,20 @@ def test_kernel_spans_and_clocks_are_recorded():
     c.close()
 
 
-@pytest.mark.parametrize("waves", ["1", "2", "2g"])
+@pytest.mark.parametrize("waves", ["1", "2", "2s"])
 @pytest.mark.parametrize("bin_bytes", ["0", "60000", "1000000000000"])
 @pytest.mark.parametrize("ref_ids", [False, True])
-def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
+def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, knob):
     """Hash bins (a quad hashes every segment of a file of at most bin_bytes back to back,
     lpt_order_block): digests, and with PFSCDC_OPT_REF_IDS the per-segment Ref.Ids, equal to
     the oracle whether no file, some files or every file forms a bin (empty files and files
     cut into many segments included); at two waves per SIMD the hash launch also runs the
-    fair-share issue priority (its launch-wide counter and the capped quiet countdown); "2g":
-    the graded fair share (PFSCDC_HASH_FAIR_GRADED) with a short interval."""
-    monkeypatch.setenv("PFSCDC_HASH_BIN_BYTES", bin_bytes)
-    monkeypatch.setenv("PFSCDC_HASH_WAVES", waves[0])
-    if waves == "2g":
-        monkeypatch.setenv("PFSCDC_HASH_FAIR_GRADED", "1")
-        monkeypatch.setenv("PFSCDC_HASH_FAIR_EVERY", "16")
+    fair-share issue priority (its launch-wide counter and the capped quiet countdown); "2s":
+    the fair share updated every 16 blocks (the PFSCDC_HASH_FAIR_EVERY knob)."""
+    knob("PFSCDC_HASH_BIN_BYTES", bin_bytes)
+    knob("PFSCDC_HASH_WAVES", waves[0])
+    if waves == "2s":
+        knob("PFSCDC_HASH_FAIR_EVERY", 16)
     rng = np.random.default_rng(5)
     lens = np.concatenate([rng.integers(0, 70_000, 200), [0, 0, 1, 30_000, 250_000, 0]])
     rng.shuffle(lens)
@@ -358,12 +364,9 @@ def test_hash_bins_equal_oracle(bin_bytes, ref_ids, waves, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("form", ["0", "1"])
-def test_scan_forms_equal_oracle(form, monkeypatch):
-    """Both forms of the narrow scan: one position per 64-bit rotation (32 copies of T) and
-    pairs of positions per rotation by 2 (16 copies of {T, rotl(T, 1)}, PFSCDC_SCAN_PAIR=1):
-    every mask width, edge sizes, dense tiles, periodic data and the reference parameters."""
-    monkeypatch.setenv("PFSCDC_SCAN_PAIR", form)
+def test_scan_edge_layouts_equal_oracle():
+    """The narrow scan at every mask width, edge sizes, dense tiles, periodic data and the
+    reference parameters."""
     for bits in (1, 4, 9, 20, 23, 31, 32):
         p = Ch.Params(average_bits=bits, seed=bits % 3, min=100, max=4000)
         offs = np.array([0, 70_000, 70_001, 200_000, 263_000], dtype=np.uint64)

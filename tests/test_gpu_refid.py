@@ -122,12 +122,11 @@ def test_get_chunks_device_resident_roundtrip_of_scan_refs():
 
 # ---------------------------------------------------------------- chunk formation + Create
 
-@pytest.mark.parametrize("split", ["0", "1", "1-lane"])
-def test_create_refs_matches_oracle_with_known_hashes(split, monkeypatch):
-    # split "1": ChaCha20 pass (coalesced: keystream parked in LDS, 16-byte pieces per lane)
-    # + BLAKE2b of the ciphertext; "1-lane": the per-lane ChaCha20 pass; "0": the fused pass
-    monkeypatch.setenv("PFSCDC_REFID_SPLIT", split[0])
-    monkeypatch.setenv("PFSCDC_CHACHA_COALESCED", "0" if split.endswith("lane") else "1")
+@pytest.mark.parametrize("split", [0, 1])
+def test_create_refs_matches_oracle_with_known_hashes(split, knob):
+    # split 1: ChaCha20 pass (coalesced: keystream parked in LDS, 16-byte pieces per lane)
+    # + BLAKE2b of the ciphertext; 0: the fused pass
+    knob("PFSCDC_REFID_SPLIT", split)
     rng = np.random.default_rng(21)
     lens = [0, 1, 63, 64, 65, 127, 128, 129, 5000, (3 << 20) + 5] + \
         list(rng.integers(1, 400_000, 60))

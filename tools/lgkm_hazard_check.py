@@ -8,7 +8,13 @@ at once, so under register pressure it may copy or spill an in-flight destinatio
 wait: a silent race (stale table entries, wrong cuts that change from run to run).  This
 walks each function of the device assembly in order, keeps the LDS ops in flight (LDS
 returns in issue order; SMEM would break the count, so any s_load makes the check demand
-lgkmcnt(0) before its use) and flags a read or write of an in-flight destination register.
+lgkmcnt(0) before its use) and flags a read or write of an in-flight destination register
+of a read issued from inline asm (between ;;#ASMSTART and ;;#ASMEND).  The compiler's own
+LDS reads count in lgkmcnt like any other, but their registers are never flagged: the
+compiler tracks those itself (SIInsertWaitcnts), and the walk is linear in text order, so
+out-of-line blocks the compiler places after a read (reached from elsewhere) would otherwise
+look like uses of its destination.  A snippet without ASMSTART markers (the self-test) is
+treated as asm throughout.
 
 usage: lgkm_hazard_check.py FILE.s [function-substring ...]   (exit 1 on a hazard)
 """
@@ -29,9 +35,17 @@ def regs(text):
 
 
 def check_function(name, lines):
-    inflight = []  # [(dest regs, line no, text)] in issue order
+    inflight = []  # [(dest regs, line no, text)] in issue order (dest empty: count only)
     hazards = []
+    has_markers = any(";;#ASMSTART" in raw for _, raw in lines)
+    in_asm = not has_markers
     for no, raw in lines:
+        if has_markers and ";;#ASMSTART" in raw:
+            in_asm = True
+            continue
+        if has_markers and ";;#ASMEND" in raw:
+            in_asm = False
+            continue
         line = raw.split(";")[0].strip()
         if not line or line.endswith(":") or line.startswith("."):
             continue
@@ -54,7 +68,7 @@ def check_function(name, lines):
                 hazards.append((no, raw.strip(), at, text, sorted(both)))
         if op.startswith("ds_read") or op.startswith("ds_load"):
             dst = args.split(",")[0]
-            inflight.append((regs(dst), no, raw.strip()))
+            inflight.append((regs(dst) if in_asm else set(), no, raw.strip()))
         elif op.startswith(("ds_write", "ds_store", "ds_bpermute", "ds_swizzle", "ds_add",
                             "s_load", "s_buffer_load", "ds_")):
             # an LDS/SMEM op without a tracked destination still counts in lgkmcnt
