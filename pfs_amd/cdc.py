@@ -449,8 +449,22 @@ def synthetic_piece_bytes(file_id: int, start: int, n: int, seed: int,
     pfscdc_fill_synthetic_pieces for one piece)."""
     if n == 0:
         return np.zeros(0, dtype=np.uint8)
-    offs = np.array([0] * (file_id + 1) + [start + n], dtype=np.uint64)  # earlier files empty
-    return synthetic_bytes(offs, seed, mode)[start:start + n]
+
+    def words(fid, a, m):  # bytes [a, a + m) of the word sequence of synthetic file fid
+        return _synth_words(fid, a >> 3, ((a & 7) + m + 7) >> 3, seed)[a & 7:(a & 7) + m]
+
+    if mode == SYNTH_DEDUP_FILES:
+        h = _mix64((seed << 48) ^ (file_id << 24) ^ 0x5EEDF11E)
+        return words(_POOL_FILE + ((h >> 1) & 63) if h & 1 else file_id, start, n)
+    if mode == SYNTH_DEDUP_BLOCKS:
+        out = np.empty(n, dtype=np.uint8)
+        for k in range(start >> 20, ((start + n - 1) >> 20) + 1):
+            b0, b1 = max(start, k << 20), min(start + n, (k + 1) << 20)
+            h = _mix64((seed << 48) ^ (file_id << 24) ^ k ^ 0xC5C5C5C5)
+            out[b0 - start:b1 - start] = (words(_POOL_FILE + ((h >> 1) & 63), b0 - (k << 20),
+                                                b1 - b0) if h & 1 else words(file_id, b0, b1 - b0))
+        return out
+    return words(file_id, start, n)
 
 
 def synthetic_bytes(file_offsets: Sequence[int], seed: int, mode: int = SYNTH_RANDOM) -> np.ndarray:
