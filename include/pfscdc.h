@@ -454,9 +454,11 @@ int pfscdc_uw_destroy(pfscdc_uwriter* w);
 const char* pfscdc_uw_last_error(const pfscdc_uwriter* w);
 /* Where the writer's time went (ms, summed over its Puts and its group writes; a group
  * write runs on a background thread while Puts continue (PFSCDC_UW_WORKERS > 1: several
- * groups in flight, each on a ctx of its own), so the stages overlap the Puts: out[0] the Puts' host copies into the fileset
- * arenas; per grouped close of the data streams out[1] the H2D upload queued, out[2] the
- * cuts-only scan (it waits for the upload), out[3] the chunk replay, out[4] the one BLAKE2b
+ * groups in flight, each on a ctx of its own), so the stages overlap the Puts: out[0] the
+ * Puts' host copies into the fileset arenas; per grouped close of the data streams out[1] the
+ * upload (until the Puts' uploads into the arena mirrors have landed, then the gathers
+ * queued; without mirrors the H2D copies queued), out[2] the cuts-only scan (without mirrors
+ * it waits for the H2D copies), out[3] the chunk replay, out[4] the one BLAKE2b
  * launch over every piece and multi-piece chunk, out[5] chunk.Create (dek, ChaCha20, Ref.Id),
  * out[6] the data chunks' callbacks; out[7] the index writers; out[8] the group writes'
  * wall time. */

@@ -681,6 +681,10 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n, double* stage_ms,
     }
   }
   if (!rc && trace && hipStreamSynchronize(st) != hipSuccess) rc = PFSCDC_EHIP;  // exact stages
+  // the Puts' uploads into the arena mirrors landed: the upload stage ends there, so the scan
+  // stage is the scan's own (the scan would wait for them on the stream anyway)
+  for (size_t e = 0; e < n_wait && !rc; e++)
+    if (hipEventSynchronize(wait_events[e]) != hipSuccess) rc = PFSCDC_EHIP;
   const auto t1 = now();
   // cut positions only: the DataRef hashes join the chunk content hashes in one launch below
   // (the commit data plane's pfscdc_commit_refs order), so their two sets of serial BLAKE2b

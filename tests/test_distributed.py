@@ -1,4 +1,4 @@
-"""Multi-rank logic on CPU (gloo, world_size 2, 3 and 4): every sharded form of the path
+"""Multi-rank logic on CPU (gloo, world_size 2, 3, 4 and 8): every sharded form of the path
 produces exactly the single-process result.  On the GPU box the same code runs over RCCL
 ("nccl" backend) from bench.py; here the per-rank compute is the CPU oracle standing in for
 the GPU (the sharding, the collectives and the border copies are what is under test).
@@ -116,7 +116,7 @@ def _files_rank_root(rank, world):
     return got.tobytes(), st, (b, e)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_gather_index_to_root_moves_live_records_only(world):
     from pfs_amd import _lib
 
@@ -326,7 +326,8 @@ def _stream_rank(rank, world, kind):
     return segs.tobytes()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "random"), (3, "random"), (3, "zeros")])
+@pytest.mark.parametrize("world,kind", [(2, "random"), (3, "random"), (3, "zeros"),
+                                        (8, "random"), (8, "zeros")])
 def test_split_stream_equals_single_scan(world, kind):
     from pfs_amd import _lib
 
@@ -338,6 +339,15 @@ def test_split_stream_equals_single_scan(world, kind):
         assert np.array_equal(got[f], want[f]), f
     if kind == "zeros":
         assert (want["size"] == P.max).sum() >= 10  # forced cuts straddle the borders
+    # the bench's own check of a split stream's line (benchkit.parity) passes on it
+    from benchkit import parity
+    from pfs_amd.cdc import ChunkParams
+    ranges = pd.split_stream(len(data), world)
+    seed = 0xC3
+    r = parity.stream_border_parity(got, len(data), ranges, seed,
+                                    ChunkParams(P.average_bits, P.seed, P.min, P.max))
+    if kind == "random":  # (the zeros run is not the synthetic stream the check regenerates)
+        assert r["gpu_equals_cpu_oracle"] and r["border_segments_checked"] >= world - 1
 
 
 def test_select_cuts_equals_oracle():
