@@ -71,7 +71,9 @@ def workload(args, world, rank):
     from pfs_amd.cdc import SYNTH_DEDUP_BLOCKS, SYNTH_DEDUP_FILES, SYNTH_RANDOM
 
     if args.config == "c2":
-        G = args.group if args.group > 0 else 32
+        # the read path holds three copies of the step (stored, ciphertext, decrypted): 16
+        # batches (3 x 64 GiB) fit in HBM, 32 do not
+        G = args.group if args.group > 0 else (16 if args.path == "get" else 32)
         n = args.files * G
         seed = 0xC2 if args.seed < 0 else args.seed
         info = {"workload": "configs[1]: batches of %d x %d B independent buffers; %d batches "

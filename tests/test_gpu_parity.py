@@ -384,3 +384,47 @@ def test_scan_edge_layouts_equal_oracle():
     offs = np.array([0, 3 << 20, (3 << 20) + 12345, (12 << 20) + 7, 22 << 20], dtype=np.uint64)
     data = synthetic_bytes(offs, 12)
     assert_same(chunker_for(DEFAULT).scan(data, offs), data, offs, DEFAULT)
+
+
+def _fuzz_layout(rng, min_, total_cap):
+    """Random batch: runs of empty, tiny (crowding a unit), sub-min, around-min, unit-sized and
+    multi-MB files in random order, up to total_cap bytes."""
+    U = 262_144
+    kinds = [lambda: 0, lambda: int(rng.integers(1, 2_000)), lambda: int(rng.integers(1, min_)),
+             lambda: int(min_ + rng.integers(-3, 4)), lambda: int(U + rng.integers(-70, 70)),
+             lambda: int(rng.integers(min_, 6 * min_)), lambda: int(rng.integers(2 << 20, 9 << 20))]
+    lens, total = [], 0
+    while total < total_cap:
+        k = int(rng.integers(0, len(kinds)))
+        run = int(rng.integers(1, 200 if k <= 1 else 6))
+        for _ in range(run):
+            n = max(0, kinds[k]())
+            lens.append(n)
+            total += n
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_cut_skip_random_layouts_equal_oracle(knob, case):
+    """Randomised layouts and parameters where the cut-skipping plan is in force (min - 1 at
+    least one 256 KiB unit): mixed runs of empty, tiny, sub-min, around-min, unit-sized and
+    long files, some files holding constant runs (candidates everywhere or nowhere), on one,
+    three or all scan workgroups.  Cuts and digests must equal the oracle's."""
+    rng = np.random.default_rng(9000 + case)
+    min_ = int(rng.integers(262_145, 1_500_000))
+    max_ = int(min_ * rng.uniform(1.2, 6.0))
+    bits = int(rng.choice([13, 15, 17, 19, 20, 23]))
+    grid = ["1", "3", ""][case % 3]
+    if grid:
+        knob("PFSCDC_SCAN_GRID", grid)
+    p = Ch.Params(average_bits=bits, seed=int(rng.integers(0, 3)), min=min_, max=max_)
+    offs = _fuzz_layout(rng, min_, 40 << 20)
+    data = synthetic_bytes(offs, 500 + case)
+    for f in rng.choice(len(offs) - 1, size=min(6, len(offs) - 1), replace=False):
+        a, b = int(offs[f]), int(offs[f + 1])
+        if b - a > 1000:
+            s = int(rng.integers(a, b - 500))
+            data[s:s + int(rng.integers(500, min(b - s, 3 << 20) + 1))] = int(rng.integers(0, 256))
+    c = chunker_for(p)
+    assert_same(c.scan(data, offs), data, offs, p)
+    assert c.last_scan_mode() & _lib.SCAN_SKIPPED_FIRST_MIN
