@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the exp/ builds it compares were deleted after the rejection; the two-frame
+# patch is in profiles/r5/rejected/scan_two_frames/.)
 # The two-frame narrow scan (round 5): same-box A/B on the default line, alternating.
 # O / O8 = the one-frame form at 3 / 2 waves per SIMD; N8 = two frames, masked keys, 2 waves
 # per SIMD (at 3 the ring needs two register sets and spills); X3 / X2 = two frames with the

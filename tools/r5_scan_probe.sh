@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the PFS_EXP_ROT_ODD / PFS_EXP_COPIES16 builds it ran were deleted with the form;
+# the two-frame patch is in profiles/r5/rejected/scan_two_frames/.)
 # Timing-only probe of a pair-rotation scan form (wrong digests in B/C/D; only the scan's
 # duration and clock matter): A = product; B = 16 table copies in use (2-way LDS bank
 # conflicts); C = B + the state rotated at odd positions only (the VALU count of a form that
