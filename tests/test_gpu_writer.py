@@ -133,3 +133,28 @@ def test_writer_write_before_annotate_is_error():
     w = st.new_writer("w", None)
     with pytest.raises(_lib.PfsCdcError):
         w.write(b"abc")
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_writer_random_streams_equal_oracle(case):
+    """Randomised annotation streams: parameters, file lengths (empty files, files around min,
+    avg and max), writer batch sizes and the number of Write calls per file all drawn from a
+    seed; every callback must equal the restated Writer's."""
+    rng = np.random.default_rng(7000 + case)
+    bits = int(rng.integers(8, 15))
+    mn = int(rng.integers(64, 6000))
+    mx = mn + int(rng.integers(1, 8 * (1 << bits)))
+    p = Ch.Params(average_bits=bits, seed=int(rng.integers(0, 4)), min=mn, max=mx)
+    kinds = [0, 1, mn - 1, mn, mn + 1, 1 << bits, (1 << bits) + 1, mx - 1, mx, mx + 1]
+    lens = []
+    for _ in range(int(rng.integers(5, 60))):
+        lens.append(int(rng.choice(kinds)) if rng.random() < 0.4 else int(rng.integers(0, 3 * mx)))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 40 + case)
+    files = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+    batch = int(rng.choice([2_000, 37_000, 1 << 20, 1 << 30]))
+    got, nchunks, nann = run_gpu(files, p, batch_bytes=batch,
+                                 writes_per_file=int(rng.integers(1, 5)))
+    want, want_n = run_oracle(files, p)
+    assert nchunks == want_n and nann == len(files)
+    assert got == want
