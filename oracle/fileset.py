@@ -263,6 +263,15 @@ class IndexWriter:
             if cw.annotation_count == 1 and cw.chunk_count == 1:
                 break
             i += 1
+        # A level above the one Close stopped at is never closed.  If it was cut while being
+        # written (its one entry at or above the index min), the reference runs that chunk's
+        # callback, which overwrites the root once closed is set, concurrently with Close's
+        # return (index/writer.go:117-123, 148-161): the outcome is a race, so refuse it.
+        # Unreachable with the reference's parameters (entries ~100 KB at most, index min 1 MB).
+        for lw in self.levels[i + 1:]:
+            if lw[0].chunk_count:
+                raise RuntimeError("index level above the closed top was cut while written "
+                                   "(the reference races its callback against Close)")
         return self.root
 
 

@@ -195,3 +195,51 @@ def test_trim_cache_frees_pooled_arenas_and_writers_still_agree():
     assert lib.pfscdc_uw_cached_arena_bytes() == 0
     want, got, wlog, glog = run_both(ops, SMALL, 400_000, SMALL_INDEX)
     check(want, got, wlog, glog)
+
+
+def random_ops(rng, data, nops, paths, thr):
+    """Random Put/delete sequence: appends and overwrites of a small path set (so paths repeat
+    across filesets), tags, empty Puts, Puts sized to the threshold, file and directory
+    deletes."""
+    ops, pos = [], 0
+    for _ in range(nops):
+        r = rng.random()
+        path = paths[int(rng.integers(0, len(paths)))]
+        if r < 0.12:
+            ops.append(("delete", path, ""))
+        elif r < 0.17:
+            ops.append(("delete", path[:path.rindex("/") + 1], ""))
+        else:
+            k = rng.random()
+            n = 0 if k < 0.1 else thr if k < 0.15 else thr // 2 if k < 0.2 else \
+                int(rng.integers(1, thr // 3))
+            n = min(n, len(data) - pos)
+            tag = ["", "default", "t1"][int(rng.integers(0, 3))]
+            ops.append(("put", path, tag, bool(rng.integers(0, 3) == 0), data[pos:pos + n]))
+            pos += n
+    return ops
+
+
+# Index chunking for the randomised workloads: min above the largest possible entry (a file
+# piece is at most memThreshold = 400 KB, so at most ~200 DataRefs at SMALL's 2,000-byte min,
+# ~20 KB encoded).  An entry at or above the index min can be cut inside the level above a
+# level that closed with one annotation in one chunk, i.e. inside a level Close never closes;
+# the reference then races that level's callback against Close's return (index/writer.go:100,
+# 121-123, 148-161).  With the reference's parameters an entry is at most ~100 KB (1e9-byte
+# filesets of >= 1 MB chunks) against a 1 MB index min, so it never happens; DESIGN §5.
+RAND_INDEX = Ch.Params(average_bits=16, seed=0, min=40_000, max=400_000)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_unordered_writer_random_ops_equal_oracle(case):
+    """Randomised Put/delete sequences against the restated UnorderedWriter (memThreshold
+    splits, exact fills, appends, overwrites, tags, file and directory deletes), with index
+    chunking small enough for several levels."""
+    rng = np.random.default_rng(3100 + case)
+    thr = int(rng.integers(60_000, 400_000))
+    data = synthetic_bytes([0, 6 << 20], 90 + case).tobytes()
+    paths = [f"/d{int(rng.integers(0, 3))}/s{int(rng.integers(0, 2))}/f{j:03d}"
+             for j in range(int(rng.integers(3, 40)))]
+    ops = random_ops(rng, data, int(rng.integers(20, 160)), paths, thr)
+    want, got, wlog, glog = run_both(ops, SMALL, thr, RAND_INDEX)
+    check(want, got, wlog, glog)
