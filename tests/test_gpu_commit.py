@@ -250,3 +250,40 @@ def test_ciphertext_in_place_whatever_the_refid_form(refid_split, knob):
     for i in range(len(coffs) - 1):
         c = ct[int(coffs[i]):int(coffs[i + 1])].tobytes()
         assert hashlib.blake2b(c, digest_size=32).digest() == bytes(refs[i]["id"]), i
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_commit_random_layouts_equal_oracle(knob, case):
+    """Randomised commits: parameters, file lengths (empty, around min and max, multi-MB),
+    stream borders (empty streams included) and the commit's forms (one or two chunk sets,
+    fused or split Ref.Id pass) drawn per case.  Chunk boundaries equal the restated Writer's
+    per stream, every chunk's content hash equals hashlib's, and a sample of Ref.Ids the
+    oracle's chunk.Create."""
+    rng = np.random.default_rng(4400 + case)
+    bits = int(rng.integers(12, 17))
+    mn = int(rng.integers(1000, 20_000))
+    p = Ch.Params(average_bits=bits, seed=int(rng.integers(0, 3)), min=mn,
+                  max=mn + int(rng.integers(1, 6 * (1 << bits))))
+    knob("PFSCDC_COMMIT_TWO_SETS", int(rng.integers(-1, 2)))
+    knob("PFSCDC_REFID_SPLIT", int(rng.integers(-1, 2)))
+    kinds = [0, 1, p.min - 1, p.min, p.max, p.max + 1, 1 << bits]
+    lens = [int(rng.choice(kinds)) if rng.random() < 0.3 else
+            int(rng.integers(0, 2 * p.max if rng.random() < 0.8 else 30 * p.max))
+            for _ in range(int(rng.integers(20, 200)))]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 700 + case)
+    nf = len(lens)
+    inner = sorted(int(x) for x in rng.integers(0, nf + 1, int(rng.integers(0, 5))))
+    streams = [0] + inner + [nf]
+    coffs, known, refs, chash, _ = both_ways(p, offs, streams, data)
+    want = []
+    for a, b in zip(streams[:-1], streams[1:]):
+        files = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(a, b)]
+        want += [len(ch.data) for ch in Ch.chunk_stream(files, p)] if files else []
+    assert np.diff(coffs).tolist() == want
+    for i in range(len(coffs) - 1):
+        chunk = data[int(coffs[i]):int(coffs[i + 1])].tobytes()
+        assert bytes(chash[i]) == hashlib.blake2b(chunk, digest_size=32).digest(), i
+    for i in np.linspace(0, len(coffs) - 2, 8).astype(int):
+        rid, dek = Ch.create_ref_id(data[int(coffs[i]):int(coffs[i + 1])].tobytes())
+        assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek, i
