@@ -230,13 +230,19 @@ def random_ops(rng, data, nops, paths, thr):
 RAND_INDEX = Ch.Params(average_bits=16, seed=0, min=40_000, max=400_000)
 
 
-@pytest.mark.parametrize("case", range(6))
-def test_unordered_writer_random_ops_equal_oracle(case):
+@pytest.mark.parametrize("case", range(8))
+def test_unordered_writer_random_ops_equal_oracle(case, knob):
     """Randomised Put/delete sequences against the restated UnorderedWriter (memThreshold
     splits, exact fills, appends, overwrites, tags, file and directory deletes), with index
-    chunking small enough for several levels."""
+    chunking small enough for several levels, and the writer's own forms drawn per case
+    (group writers, group size, upload during the Puts, grouped index closes): none may
+    change a result."""
     rng = np.random.default_rng(3100 + case)
     thr = int(rng.integers(60_000, 400_000))
+    knob("PFSCDC_UW_WORKERS", int(rng.integers(1, 3)))
+    knob("PFSCDC_UW_INFLIGHT", int(rng.choice([1 << 35, 3 * thr, 700_000])))
+    knob("PFSCDC_UW_MIRROR", int(rng.integers(0, 2)))
+    knob("PFSCDC_UW_INDEX_GROUPED", int(rng.integers(0, 2)))
     data = synthetic_bytes([0, 6 << 20], 90 + case).tobytes()
     paths = [f"/d{int(rng.integers(0, 3))}/s{int(rng.integers(0, 2))}/f{j:03d}"
              for j in range(int(rng.integers(3, 40)))]
