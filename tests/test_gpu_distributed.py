@@ -65,6 +65,33 @@ def test_split_stream_primitives_equal_scan(world):
     ch.close()
 
 
+@pytest.mark.parametrize("case", range(6))
+def test_split_stream_random_borders_equal_scan(case):
+    """Randomised single streams split over 1-8 virtual ranks: length, parameters and
+    constant runs (candidates everywhere or nowhere, forced cuts) drawn per case; the
+    gathered candidates equal the oracle's, and the selected segments and digests one scan's."""
+    rng = np.random.default_rng(5500 + case)
+    n = int(rng.integers(300_000, 9_000_000))
+    bits = int(rng.integers(9, 15))
+    mn = int(rng.integers(64, 8000))
+    p = Ch.Params(average_bits=bits, seed=int(rng.integers(0, 3)), min=mn,
+                  max=mn + int(rng.integers(1, 8 * (1 << bits))))
+    world = int(rng.integers(1, 9))
+    data = synthetic_bytes([0, n], 600 + case)
+    for _ in range(int(rng.integers(0, 4))):
+        a = int(rng.integers(0, n))
+        data[a:a + int(rng.integers(1, 400_000))] = int(rng.integers(0, 256))
+    dev = torch.from_numpy(data).cuda()
+    ch = Chunker(cp(p))
+    cands, offs, sizes, flags, digests = split_scan(ch, dev, n, world, p)
+    assert np.array_equal(cands, coracle.candidates(data, p, cap=1 << 24))
+    segs = ch.scan(dev, [0, n]).segments
+    assert np.array_equal(segs["offset"], offs) and np.array_equal(segs["size"], sizes)
+    assert np.array_equal(segs["flags"], flags)
+    assert np.array_equal(segs["hash"], digests)
+    ch.close()
+
+
 def test_candidates_dense_tiles_and_halo():
     # avgBits 3: ~1 candidate per 8 bytes, every tile dense (re-rolled on the host)
     p = Ch.Params(average_bits=3, seed=1, min=64, max=5000)
