@@ -167,3 +167,65 @@ def test_copy_of_tampered_chunk_fails_verification():
         w.copy(d)  # the first chunk is an edge chunk: read back (chunk.Get verifyData)
         w.close()
     assert e.value.code == -7
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_copy_random_plans_match_oracle(case):
+    """Randomised Copy streams: stored files of random sizes (empty included), a random plan
+    of copies (any order, repeats) and written files, a random writer batch size; every
+    callback equal to the restated Writer.Copy's."""
+    rng = np.random.default_rng(6600 + case)
+    sizes = [0 if rng.random() < 0.1 else int(rng.integers(1, 60_000))
+             for _ in range(int(rng.integers(2, 12)))]
+    parts, _ = parts_of(20 + case, sizes)
+    store = pc.ChunkStore()
+    _, per_file = gpu_write(parts, store)
+    ostore = {}
+    _, oper_file = oracle_write(parts, ostore)
+    extra, _ = parts_of(40 + case, [int(rng.integers(0, 30_000)) for _ in range(4)])
+    plan = [("copy", int(rng.integers(0, len(parts)))) if rng.random() < 0.7 else
+            ("write", int(rng.integers(0, len(extra)))) for _ in range(int(rng.integers(3, 16)))]
+    batch = int(rng.choice([1 << 30, 2_500, 20_000]))
+    got, want = [], []
+    st = pc.Storage(0, batch, store=store)
+    w = st.new_writer("w2", lambda anns: got.append([_key(a) for a in anns]),
+                      pc.with_rolling_hash_config(P.average_bits, P.seed),
+                      pc.with_min_max(P.min, P.max))
+    ow = Ch.Writer(cb=lambda anns: want.append([_key(a) for a in anns]), params=P, store=ostore)
+    for k, (op, i) in enumerate(plan):
+        w.annotate(pc.Annotation(data=k))
+        ow.annotate(Ch.Annotation(data=k))
+        if op == "write":
+            w.write(extra[i])
+            ow.write(extra[i])
+        else:
+            for d in per_file.get(i, []):
+                w.copy(d)
+            for d in copy.deepcopy(oper_file.get(i, [])):
+                ow.copy(d)
+    w.close()
+    ow.close()
+    assert got == want
+    assert w.chunk_count() == ow.chunk_count
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_stable_hash_random_splits(case):
+    """TestStableHash with random uneven split points: the merged hash of the pieces' DataRefs
+    equals the single writer's, on the GPU and in the oracle."""
+    rng = np.random.default_rng(7700 + case)
+    n = int(rng.integers(20_000, 300_000))
+    data = synthetic_bytes([0, n], 30 + case).tobytes()
+    store = pc.ChunkStore()
+    _, pf = gpu_write([data], store)
+    single = pc.hash_data_refs([d.hash for d in pf[0]], params=CP)
+    cuts = sorted(set(int(x) for x in rng.integers(1, n, int(rng.integers(1, 9)))))
+    bounds = [0] + cuts + [n]
+    refs, orefs, ostore = [], [], {}
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        _, p = gpu_write([data[a:b]], store)
+        refs += p.get(0, [])
+        _, op = oracle_write([data[a:b]], ostore)
+        orefs += op.get(0, [])
+    assert Ch.merge_file_hash(ostore, copy.deepcopy(orefs), P) == single
+    assert pc.merge_file_hash(store, refs, params=CP) == single
