@@ -428,3 +428,32 @@ def test_cut_skip_random_layouts_equal_oracle(knob, case):
     c = chunker_for(p)
     assert_same(c.scan(data, offs), data, offs, p)
     assert c.last_scan_mode() & _lib.SCAN_SKIPPED_FIRST_MIN
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_reference_params_random_batches_equal_oracle(case):
+    """The reference's parameters (avgBits 23, min 1,000,000, max 20,000,000) on random
+    batches of ~100-200 MB: file lengths around min and max and the 256 KiB unit, tiny files,
+    multi-max files, constant runs that force cuts at max or make every position a
+    candidate; cuts and digests equal the oracle's, with the cut-skipping plan in force."""
+    rng = np.random.default_rng(8800 + case)
+    kinds = [0, 1, 999_999, 1_000_000, 1_000_001, 262_144, 19_999_999, 20_000_000, 20_000_001,
+             4 << 20, 10_737_418]
+    lens, total = [], 0
+    while total < int(rng.integers(100, 200)) << 20:
+        k = rng.random()
+        if k < 0.2:  # a run of tiny files (crowding a scan unit)
+            run = [int(x) for x in rng.integers(0, 3000, int(rng.integers(1, 150)))]
+            lens += run
+            total += sum(run)
+            continue
+        n = int(rng.choice(kinds)) if k < 0.6 else int(rng.integers(0, 25_000_000))
+        lens.append(n)
+        total += n
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 900 + case)
+    for _ in range(int(rng.integers(1, 4))):
+        a = int(rng.integers(0, total))
+        data[a:a + int(rng.integers(1, 30_000_000))] = int(rng.integers(0, 256))
+    c = chunker_for(DEFAULT)
+    assert_same(c.scan(data, offs), data, offs, DEFAULT)
