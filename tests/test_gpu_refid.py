@@ -182,3 +182,41 @@ def test_form_chunks_and_refs_match_writer_streams(streams):
     for i, ch in enumerate(want):
         rid, dek = Ch.create_ref_id(ch.data)
         assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek, i
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_get_chunks_random_tampering(case):
+    """chunk.Get (verify BLAKE2b(stored) == Ref.Id, then decrypt) on random chunk sizes with
+    a random subset damaged: a flipped stored byte anywhere (first, last, inside a partial
+    final block) or a Ref.Id that names other bytes.  Exactly the damaged chunks fail, and
+    every other chunk decrypts to its plaintext."""
+    rng = np.random.default_rng(9900 + case)
+    lens = [int(rng.choice([0, 1, 127, 128, 129, 255, 256, 257])) if rng.random() < 0.3 else
+            int(rng.integers(1, 200_000)) for _ in range(int(rng.integers(10, 60)))]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    plain = synthetic_bytes(offs, 50 + case)
+    chunks = [plain[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+    ctexts, refs = _encrypt(chunks)
+    stored = np.frombuffer(b"".join(ctexts), dtype=np.uint8).copy()
+    orig, refs = refs, refs.copy()
+    bad = set()
+    for i in range(len(lens)):
+        if lens[i] == 0 or rng.random() > 0.3:
+            continue
+        bad.add(i)
+        if rng.random() < 0.7:
+            pos = int(rng.choice([0, lens[i] - 1, int(rng.integers(0, lens[i]))]))
+            stored[int(offs[i]) + pos] ^= 1 << int(rng.integers(0, 8))
+        else:
+            refs[i]["id"] = refs[(i + 1) % len(lens)]["id"] if lens[(i + 1) % len(lens)] \
+                else np.frombuffer(bytes(32), dtype=np.uint8)
+            if bytes(refs[i]["id"]) == bytes(orig[i]["id"]):
+                bad.discard(i)  # an identical neighbour: the id still names these bytes
+    c = Chunker(ChunkParams(), 0)
+    pt, ok = c.get_chunks(stored, offs, refs)
+    assert set(np.flatnonzero(~ok.astype(bool)).tolist()) == bad
+    for i in range(len(lens)):
+        if i not in bad:
+            assert np.array_equal(pt[int(offs[i]):int(offs[i + 1])],
+                                  plain[int(offs[i]):int(offs[i + 1])]), i
+    c.close()
