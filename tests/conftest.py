@@ -38,3 +38,12 @@ def knob():
     yield set_
     for k, v in old.items():
         _lib.set_knob(k, v)
+
+
+def fuzz_cases(default: int):
+    """Seeds of a randomised parity test: range(default), or range(PFS_FUZZ_CASES) for a
+    longer soak (PFS_FUZZ_CASES=60 python -m pytest -m gpu -k random ...)."""
+    import os
+
+    n = os.environ.get("PFS_FUZZ_CASES")
+    return range(int(n) if n else default)

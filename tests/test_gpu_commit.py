@@ -9,6 +9,8 @@ import hashlib
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from pfs_amd.cdc import ChunkParams, Chunker, synthetic_bytes
 
@@ -252,7 +254,7 @@ def test_ciphertext_in_place_whatever_the_refid_form(refid_split, knob):
         assert hashlib.blake2b(c, digest_size=32).digest() == bytes(refs[i]["id"]), i
 
 
-@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("case", fuzz_cases(6))
 def test_commit_random_layouts_equal_oracle(knob, case):
     """Randomised commits: parameters, file lengths (empty, around min and max, multi-MB),
     stream borders (empty streams included) and the commit's forms (one or two chunk sets,

@@ -13,6 +13,8 @@ import sys
 
 import numpy as np
 import pytest
+
+from conftest import fuzz_cases
 import torch
 
 from oracle import chunker as Ch
@@ -65,7 +67,7 @@ def test_split_stream_primitives_equal_scan(world):
     ch.close()
 
 
-@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("case", fuzz_cases(6))
 def test_split_stream_random_borders_equal_scan(case):
     """Randomised single streams split over 1-8 virtual ranks: length, parameters and
     constant runs (candidates everywhere or nowhere, forced cuts) drawn per case; the

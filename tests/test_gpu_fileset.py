@@ -14,6 +14,8 @@ is run as well).
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from oracle import fileset as OF
 from pfs_amd import _lib
@@ -230,7 +232,7 @@ def random_ops(rng, data, nops, paths, thr):
 RAND_INDEX = Ch.Params(average_bits=16, seed=0, min=40_000, max=400_000)
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", fuzz_cases(8))
 def test_unordered_writer_random_ops_equal_oracle(case, knob):
     """Randomised Put/delete sequences against the restated UnorderedWriter (memThreshold
     splits, exact fills, appends, overwrites, tags, file and directory deletes), with index

@@ -9,6 +9,8 @@ import hashlib
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from oracle import coracle
 from pfs_amd import _lib
@@ -404,7 +406,7 @@ def _fuzz_layout(rng, min_, total_cap):
     return np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", fuzz_cases(16))
 def test_cut_skip_random_layouts_equal_oracle(knob, case):
     """Randomised layouts and parameters where the cut-skipping plan is in force (min - 1 at
     least one 256 KiB unit): mixed runs of empty, tiny, sub-min, around-min, unit-sized and
@@ -430,7 +432,7 @@ def test_cut_skip_random_layouts_equal_oracle(knob, case):
     assert c.last_scan_mode() & _lib.SCAN_SKIPPED_FIRST_MIN
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", fuzz_cases(4))
 def test_reference_params_random_batches_equal_oracle(case):
     """The reference's parameters (avgBits 23, min 1,000,000, max 20,000,000) on random
     batches of ~100-200 MB: file lengths around min and max and the 256 KiB unit, tiny files,

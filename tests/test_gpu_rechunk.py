@@ -12,6 +12,8 @@ import copy
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from pfs_amd import _lib
 from pfs_amd import chunk as pc
@@ -169,7 +171,7 @@ def test_copy_of_tampered_chunk_fails_verification():
     assert e.value.code == -7
 
 
-@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("case", fuzz_cases(6))
 def test_copy_random_plans_match_oracle(case):
     """Randomised Copy streams: stored files of random sizes (empty included), a random plan
     of copies (any order, repeats) and written files, a random writer batch size; every
@@ -209,7 +211,7 @@ def test_copy_random_plans_match_oracle(case):
     assert w.chunk_count() == ow.chunk_count
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", fuzz_cases(4))
 def test_stable_hash_random_splits(case):
     """TestStableHash with random uneven split points: the merged hash of the pieces' DataRefs
     equals the single writer's, on the GPU and in the oracle."""

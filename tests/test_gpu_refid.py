@@ -8,6 +8,8 @@ own writer, so every segment is one chunk."""
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from oracle import coracle
 from pfs_amd.cdc import ChunkParams, Chunker, synthetic_bytes
@@ -184,7 +186,7 @@ def test_form_chunks_and_refs_match_writer_streams(streams):
         assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek, i
 
 
-@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("case", fuzz_cases(4))
 def test_get_chunks_random_tampering(case):
     """chunk.Get (verify BLAKE2b(stored) == Ref.Id, then decrypt) on random chunk sizes with
     a random subset damaged: a flipped stored byte anywhere (first, last, inside a partial

@@ -10,6 +10,8 @@ last chunk (E1) and writer batches that split a stream across several GPU scans.
 import numpy as np
 import pytest
 
+from conftest import fuzz_cases
+
 from oracle import chunker as Ch
 from pfs_amd import chunk as pc
 from pfs_amd.cdc import synthetic_bytes
@@ -135,7 +137,7 @@ def test_writer_write_before_annotate_is_error():
         w.write(b"abc")
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", fuzz_cases(8))
 def test_writer_random_streams_equal_oracle(case):
     """Randomised annotation streams: parameters, file lengths (empty files, files around min,
     avg and max), writer batch sizes and the number of Write calls per file all drawn from a
