@@ -178,6 +178,10 @@ struct pfscdc_writer {
   // deferred flushes (Copy's buf.Len() probes): buf[0, replayed) was replayed without its
   // BLAKE2b; buf, carry and the formed chunks stay until a dispatching flush hashes them
   uint64_t replayed = 0;
+  // a deferred flush ran and nothing has dispatched since (replayed alone cannot say: a
+  // deferred flush may replay 0 bytes of buf, e.g. only the carry forming a chunk at an
+  // Annotate, and the next flush must not re-base the open chunk onto the carry again)
+  bool deferred = false;
   uint64_t dev_upto = 0;              // while deferring: buf[0, dev_upto) is already on the device
   bool buffering = false;             // Writer.buffering (Copy)
   bool closed = false;
@@ -268,25 +272,33 @@ int dispatch(pfscdc_writer* w, uint64_t valid) {
     for (size_t i = 0; i < n; i++)
       if (!cf.events[i].ref.copied) which.push_back(i);
     const size_t m = which.size();
-    w->chunk_offs.resize(m + 1);
     w->hashes.resize(32 * m);
     w->known.resize(m);
     std::vector<pfscdc_ref> refs(m);
     for (size_t k = 0; k < m; k++) {
       const ChunkEvent& ev = cf.events[which[k]];
-      w->chunk_offs[k] = ev.begin;
       w->known[k] = ev.known;
       std::memcpy(&w->hashes[32 * k], ev.hash, 32);
     }
-    if (m) w->chunk_offs[m] = cf.events[which[m - 1]].end;
     uint8_t* ct = w->upload && w->store ? w->d_ctext : nullptr;
-    if (m)
+    // one create_refs call per run of new chunks that are contiguous in the device buffer (a
+    // chunk's bytes are [offs[k], offs[k + 1]) there, so the offsets of one call must tile);
+    // the chunks of one flush normally form a single run
+    for (size_t r0 = 0; r0 < m && !rc;) {
+      size_t r1 = r0 + 1;
+      while (r1 < m && cf.events[which[r1]].begin == cf.events[which[r1 - 1]].end) r1++;
+      w->chunk_offs.resize(r1 - r0 + 1);
+      for (size_t k = r0; k < r1; k++) w->chunk_offs[k - r0] = cf.events[which[k]].begin;
+      w->chunk_offs[r1 - r0] = cf.events[which[r1 - 1]].end;
       rc = pfscdc::create_refs_device(w->ctx, w->d_buf, valid, w->chunk_offs.data(),
-                                      (uint32_t)m, w->hashes.data(), w->known.data(),
-                                      refs.data(), ct);
-    for (size_t k = 0; k < m && !rc; k++) {
-      w->refs[which[k]] = refs[k];
-      if (ct) rc = upload(w->store, refs[k], ct, w->chunk_offs[k], w->chunk_offs[k + 1]);
+                                      (uint32_t)(r1 - r0), w->hashes.data() + 32 * r0,
+                                      w->known.data() + r0, refs.data() + r0, ct);
+      for (size_t k = r0; k < r1 && !rc; k++) {
+        w->refs[which[k]] = refs[k];
+        if (ct) rc = upload(w->store, refs[k], ct, cf.events[which[k]].begin,
+                            cf.events[which[k]].end);
+      }
+      r0 = r1;
     }
     if (rc) {
       clear_events(cf);
@@ -364,7 +376,7 @@ int flush(pfscdc_writer* w, FlushMode mode) {
   const uint64_t cl = w->carry.size();
   const uint64_t base = (cl + 15) & ~15ULL;
   // while deferring, carry and buf[0, dev_upto) are already on the device: send the rest
-  const uint64_t have = R ? w->dev_upto : 0;
+  const uint64_t have = w->deferred ? w->dev_upto : 0;
   int rc = ensure_device(w, base + nbytes + 64, have ? base + have : 0);
   if (rc) return set_err(w, rc);
   if ((!have && cl && hipMemcpy(w->d_buf + base - cl, w->carry.data(), cl, hipMemcpyHostToDevice) != hipSuccess) ||
@@ -372,7 +384,7 @@ int flush(pfscdc_writer* w, FlushMode mode) {
                                   hipMemcpyHostToDevice) != hipSuccess))
     return set_err(w, PFSCDC_EHIP);
   w->dev_upto = nbytes;
-  if (R == 0) cf.open_start = base - cl;  // else unchanged since the deferred flush
+  if (!w->deferred) cf.open_start = base - cl;  // else unchanged since the deferred flush
   cf.pos = base + R;
   uint64_t consumed = nbytes;  // bytes of buf replayed
   bool keep_tail = false;
@@ -413,6 +425,7 @@ int flush(pfscdc_writer* w, FlushMode mode) {
   w->files.clear();
   if (defer) {  // everything stays: buf, carry, the formed chunks; only the tail is pending
     w->replayed = consumed;
+    w->deferred = true;
     if (keep_tail) w->files.push_back(PendingFile{tail_user, consumed, true});
     return PFSCDC_OK;
   }
@@ -432,6 +445,7 @@ int flush(pfscdc_writer* w, FlushMode mode) {
     w->carry.swap(next);
   }
   w->replayed = 0;
+  w->deferred = false;
   if (keep_tail) {
     w->buf.erase(w->buf.begin(), w->buf.begin() + consumed);
     w->files.push_back(PendingFile{tail_user, 0, true});
@@ -617,7 +631,7 @@ int writers_close_group(pfscdc_writer* const* ws, size_t n, double* stage_ms,
   for (size_t i = 0; i < n && group; i++) {
     const pfscdc_writer* w = ws[i];
     group = !w->err && !w->closed && w->ctx == ctx && !w->buffering && w->carry.empty() &&
-            w->d_cap == 0 && w->replayed == 0 && w->cf.events.empty() &&
+            w->d_cap == 0 && w->replayed == 0 && !w->deferred && w->cf.events.empty() &&
             w->ref_ids == ws[0]->ref_ids &&
             (w->upload && w->store) == (ws[0]->upload && ws[0]->store);
   }

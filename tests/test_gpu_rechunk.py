@@ -176,6 +176,21 @@ def test_copy_random_plans_match_oracle(case):
     """Randomised Copy streams: stored files of random sizes (empty included), a random plan
     of copies (any order, repeats) and written files, a random writer batch size; every
     callback equal to the restated Writer.Copy's."""
+    _copy_case(case)
+
+
+@pytest.mark.parametrize("case", [13, 23, 32, 43, 51, 55, 58])
+def test_copy_after_carry_only_probe_flush(case):
+    """Regression (round 5, found by the randomised plans): Copy's buf.Len() probe flush
+    replayed no bytes of the buffer, only the carried open chunk, which an Annotate cut into a
+    chunk (buf.Len() >= avg); whole-chunk copies followed, then written bytes.  The next flush
+    took the zero replay count for 'no deferred flush' and re-based the open chunk onto the
+    carry, so the following new chunk's Ref.Id (and upload) covered the wrong bytes (its dek
+    and DataRef hash were right).  These seeds hit it."""
+    _copy_case(case)
+
+
+def _copy_case(case):
     rng = np.random.default_rng(6600 + case)
     sizes = [0 if rng.random() < 0.1 else int(rng.integers(1, 60_000))
              for _ in range(int(rng.integers(2, 12)))]
