@@ -459,3 +459,38 @@ def test_reference_params_random_batches_equal_oracle(case):
         data[a:a + int(rng.integers(1, 30_000_000))] = int(rng.integers(0, 256))
     c = chunker_for(DEFAULT)
     assert_same(c.scan(data, offs), data, offs, DEFAULT)
+
+
+@pytest.mark.parametrize("case", fuzz_cases(8))
+def test_knobs_never_change_results(knob, case):
+    """no knob changes a result.  Random layouts and parameters under random
+    settings of every scan and hash knob at once (workgroup cap, both skips, hash bins, waves
+    per SIMD, fair share and its period), device-resident or host input."""
+    import torch
+
+    rng = np.random.default_rng(12000 + case)
+    bits = int(rng.integers(12, 24))
+    mn = int(rng.choice([2000, 70_000, 262_145, 1_000_000]))
+    p = Ch.Params(average_bits=bits, seed=int(rng.integers(0, 3)), min=mn,
+                  max=mn + int(rng.integers(1, 4 * (1 << bits) + 2)))
+    knob("PFSCDC_SCAN_GRID", int(rng.choice([0, 1, 3, 64])))
+    knob("PFSCDC_SCAN_SKIP", int(rng.integers(0, 2)))
+    knob("PFSCDC_SCAN_CUTSKIP", int(rng.integers(0, 2)))
+    knob("PFSCDC_HASH_BIN_BYTES", int(rng.choice([-1, 0, 60_000, 1 << 40])))
+    knob("PFSCDC_HASH_WAVES", int(rng.integers(0, 3)))
+    knob("PFSCDC_HASH_FAIR", int(rng.integers(0, 2)))
+    knob("PFSCDC_HASH_FAIR_EVERY", int(rng.choice([8, 16, 256, 4096])))
+    lens, total = [], 0
+    for _ in range(int(rng.integers(1, 120))):
+        n = int(rng.integers(0, min(3 * p.max, 8 << 20))) if rng.random() < 0.7 else \
+            int(rng.integers(0, 3000))
+        if total + n > 150 << 20:
+            break
+        lens.append(n)
+        total += n
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = synthetic_bytes(offs, 1200 + case)
+    c = Chunker(cp(p), device=0)
+    src = torch.from_numpy(data).cuda() if rng.random() < 0.5 else data
+    assert_same(c.scan(src, offs), data, offs, p)
+    c.close()
