@@ -494,3 +494,29 @@ def test_knobs_never_change_results(knob, case):
     src = torch.from_numpy(data).cuda() if rng.random() < 0.5 else data
     assert_same(c.scan(src, offs), data, offs, p)
     c.close()
+
+
+def test_invalid_arguments_are_refused_and_the_ctx_stays_usable():
+    """Bad offsets (not starting at 0, not ending at the byte count, decreasing), refs that do
+    not match the chunks, and unaligned device bytes are refused with an error before any
+    kernel runs; the same ctx then scans a valid batch correctly."""
+    import torch
+
+    offs = np.array([0, 5000, 90_000, 200_000], dtype=np.uint64)
+    data = synthetic_bytes(offs, 77)
+    c = Chunker(cp(SMALL), device=0)
+    bad = [[1, 5000, 90_000, 200_000], [0, 5000, 90_000, 199_999], [0, 5000, 90_000, 200_001],
+           [0, 90_000, 5000, 200_000], [200_000, 0]]
+    for b in bad:
+        with pytest.raises(_lib.PfsCdcError):
+            c.scan(data, b)
+        assert_same(c.scan(data, offs), data, offs, SMALL)
+    dev = torch.from_numpy(np.concatenate([np.zeros(1, np.uint8), data])).cuda()
+    with pytest.raises(_lib.PfsCdcError, match="aligned"):
+        c.scan(dev[1:], offs)
+    refs = np.zeros(3, dtype=_lib.ref_dtype())
+    for b in ([0, 10, 20, 200_001], [0, 20, 10, 200_000]):
+        with pytest.raises(_lib.PfsCdcError):
+            c.get_chunks(data, b, refs)
+    assert_same(c.scan(data, offs), data, offs, SMALL)
+    c.close()
