@@ -289,3 +289,20 @@ def test_commit_random_layouts_equal_oracle(knob, case):
     for i in np.linspace(0, len(coffs) - 2, 8).astype(int):
         rid, dek = Ch.create_ref_id(data[int(coffs[i]):int(coffs[i + 1])].tobytes())
         assert bytes(refs[i]["id"]) == rid and bytes(refs[i]["dek"]) == dek, i
+    if rng.random() < 0.5:  # the ciphertext written over device-resident input
+        import torch
+
+        cp = ChunkParams(p.average_bits, p.seed, p.min, p.max)
+        c = Chunker(cp, 0)
+        c.set_cuts_only(True)
+        c.set_ctext_in_place(True)
+        t = torch.from_numpy(data).to("cuda:0")
+        c.scan(t, offs)
+        coffs_c, _, known_c = c.form_chunks(streams)
+        refs_c, _, _ = c.commit_refs(t, coffs_c, known_c)
+        assert np.array_equal(refs_c["id"], refs["id"]) and np.array_equal(refs_c["dek"], refs["dek"])
+        ct = t.cpu().numpy()
+        for i in range(len(coffs) - 1):
+            blob = ct[int(coffs[i]):int(coffs[i + 1])].tobytes()
+            assert hashlib.blake2b(blob, digest_size=32).digest() == bytes(refs[i]["id"]), i
+        c.close()
