@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: PFSCDC_HASH_PRIO, the hash launches' issue priority knob it sweeps, was removed in
+# round 5 with the other rejected forms; the results are in profiles/r4/uw_sweep/.)
 # Host-fed writer (32 GiB c4 Put): group writers in flight x group size x hash issue priority,
 # after the grouped index close.  Each line: value, ms/step, stages, filesets digest.
 set -o pipefail

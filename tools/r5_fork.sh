@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: PFSCDC_HASH_FORK exists only with profiles/r5/rejected/first_piece_fork/
+# fork.patch applied; the form was rejected and removed.)
 # The first-piece fork in pfscdc_commit_refs (PFSCDC_HASH_FORK): GPU parity of the commit
 # suites, then c4 commits (G = 2) with the fork on and off alternating on one box, then the
 # host-fed writer's stages with the upload split out (mirror uploads landed vs GPU work).
