@@ -41,9 +41,11 @@ def knob():
 
 
 def fuzz_cases(default: int):
-    """Seeds of a randomised parity test: range(default), or range(PFS_FUZZ_CASES) for a
-    longer soak (PFS_FUZZ_CASES=60 python -m pytest -m gpu -k random ...)."""
+    """Seeds of a randomised parity test: range(default), or PFS_FUZZ_CASES seeds from
+    PFS_FUZZ_FIRST (default 0) for a longer soak
+    (PFS_FUZZ_CASES=60 PFS_FUZZ_FIRST=1000 python -m pytest -m gpu -k random ...)."""
     import os
 
     n = os.environ.get("PFS_FUZZ_CASES")
-    return range(int(n) if n else default)
+    first = int(os.environ.get("PFS_FUZZ_FIRST", "0"))
+    return range(first, first + (int(n) if n else default))
