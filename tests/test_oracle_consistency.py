@@ -127,3 +127,34 @@ def test_annotate_cuts_before_file_when_open_chunk_reaches_avg():
     # chunk boundaries fall exactly where the open buffer first reaches >= 4096 at Annotate
     sizes = [len(c.data) for c in chunks]
     assert sizes[:-1] == [4500, 4500] and sum(sizes) == 8 * 1500
+
+
+def test_three_oracle_forms_agree_on_random_params():
+    """Property test (hypothesis): the literal byte-by-byte Writer, the numpy closed form and
+    the C restatement agree on random parameters (mask width, seed, min, max) and random
+    file lengths, including lengths at min, max and 64 and empty files."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    @settings(max_examples=30, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(bits=st.integers(4, 12), seed=st.integers(0, 3), mn=st.integers(64, 3000),
+           extra=st.integers(1, 6000), lens=st.lists(st.integers(0, 12_000), min_size=1,
+                                                     max_size=12),
+           data_seed=st.integers(0, 1 << 30))
+    def check(bits, seed, mn, extra, lens, data_seed):
+        p = Ch.Params(average_bits=bits, seed=seed, min=mn, max=mn + extra)
+        lens = [min(x, 12_000) if x % 7 else [0, mn, mn + extra, 64][x % 4] for x in lens]
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        data = synthetic_bytes(offs, data_seed)
+        files = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(len(lens))]
+        lit = Ch.chunk_stream(files, p, "literal")
+        fast = Ch.chunk_stream(files, p, "numpy")
+        assert [(c.data, c.edge) for c in lit] == [(c.data, c.edge) for c in fast]
+        fl = Ch.file_segments_from_chunks(lit, len(files))
+        segs, begin = coracle.segment_files(data, offs, p, nthreads=2)
+        for f in range(len(files)):
+            got = [(int(s["offset"]), int(s["size"]), bytes(s["hash"]))
+                   for s in segs[int(begin[f]):int(begin[f + 1])]]
+            assert got == fl[f]
+
+    check()
