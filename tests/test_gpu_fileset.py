@@ -251,3 +251,38 @@ def test_unordered_writer_random_ops_equal_oracle(case, knob):
     ops = random_ops(rng, data, int(rng.integers(20, 160)), paths, thr)
     want, got, wlog, glog = run_both(ops, SMALL, thr, RAND_INDEX)
     check(want, got, wlog, glog)
+
+
+@pytest.mark.parametrize("case", fuzz_cases(6))
+def test_unordered_writer_tricky_paths_equal_oracle(case):
+    """Paths and tags that stress the Buffer's byte-wise (path, tag) order and the prefix
+    match of directory deletes (buffer.go:70-106, unordered_writer.go): shared prefixes of
+    different lengths ('/a', '/a/b', '/ab', '/a-b'), non-ASCII UTF-8, deep nesting, tags
+    sorting around '' and 'default', deletes of '/', of a file's own path with a trailing
+    slash, and of directories that do not exist."""
+    rng = np.random.default_rng(3300 + case)
+    atoms = ["a", "b", "ab", "a-b", "a.b", "é", "日本", "z", "A", "0", "a b"]
+    paths = []
+    for _ in range(int(rng.integers(5, 30))):
+        depth = int(rng.integers(1, 5))
+        paths.append("/" + "/".join(atoms[int(rng.integers(0, len(atoms)))] for _ in range(depth)))
+    tags = ["", "default", "Default", "t", "t0", "é"]
+    thr = int(rng.integers(30_000, 200_000))
+    data = synthetic_bytes([0, 3 << 20], 130 + case).tobytes()
+    ops, pos = [], 0
+    for _ in range(int(rng.integers(20, 100))):
+        r = rng.random()
+        path = paths[int(rng.integers(0, len(paths)))]
+        if r < 0.1:
+            ops.append(("delete", path, tags[int(rng.integers(0, len(tags)))]))
+        elif r < 0.18:
+            d = path[:path.rindex("/") + 1] if rng.random() < 0.7 else \
+                ["/", path + "/", "/nothing/"][int(rng.integers(0, 3))]
+            ops.append(("delete", d, ""))
+        else:
+            n = min(int(rng.integers(0, thr // 2)), len(data) - pos)
+            ops.append(("put", path, tags[int(rng.integers(0, len(tags)))],
+                        bool(rng.integers(0, 3) == 0), data[pos:pos + n]))
+            pos += n
+    want, got, wlog, glog = run_both(ops, SMALL, thr, RAND_INDEX)
+    check(want, got, wlog, glog)
