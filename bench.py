@@ -167,7 +167,7 @@ def hw_queues_setting(at_least: int = 8) -> int:
     """HIP streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4)
     share a queue and run one after the other: c3's streams in flight (one context each) and
     the commit's two chunk sets need a queue per stream.  Raised to
-    ``at_least`` (8; 32 for c3's twelve streams) before the first HIP call; a larger setting
+    ``at_least`` (8; 32 for c3's twenty streams) before the first HIP call; a larger setting
     is kept.  The effective value goes into the line's config."""
     try:
         q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
@@ -191,7 +191,7 @@ def main():
     c3s = c3_streams(args)
     hwq = hw_queues_setting(C3_QUEUES if c3s or args.config == "c2" else 8)
     if c3s:
-        # a step's scan takes one workgroup per CU; with up to twelve chain-bound hash launches
+        # a step's scan takes one workgroup per CU; with up to twenty chain-bound hash launches
         # of the other streams holding CUs, capped workgroups never wait for them (the
         # PFSCDC_SCAN_GRID knob, read from the environment when the library first uses a knob;
         # an explicit setting is kept)

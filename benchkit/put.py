@@ -16,8 +16,9 @@ def inflight_for(args) -> int:
     """Steps in flight.  One at a time by default, so every kernel launch has the GPU to itself
     and its duration (HIP events, in-kernel span and a kernel trace alike) is its own.  c3 (one
     stream, bound by its longest 20 MB chains: ~175 ms per stream whatever else runs) runs
-    twelve steps in flight on twelve contexts with 32 hardware queues and scans capped at 64
-    workgroups; c4/c5 two (the next commit's scan and hashes fill what the chain-bound hash
+    twenty steps in flight on twenty contexts with 32 hardware queues and scans capped at 64
+    workgroups (12/16/20 streams: 547/590/673 GiB/s, same box; 24 outrun the queues:
+    profiles/r5/c3_inflight/); c4/c5 two (the next commit's scan and hashes fill what the chain-bound hash
     leaves: 824 -> 936 / 820 -> 883 GiB/s, profiles/r3/c4_inflight/).  c2's two-in-flight
     throughput is measured after the timed region (``two_in_flight``)."""
     if args.inflight > 0:
