@@ -120,6 +120,12 @@ def parse():
                     help="skip the one-chain rate measurement (chain_floor)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="c2: skip the two-in-flight throughput leg")
+    ap.add_argument("--literal-inflight", type=int, default=0,
+                    help="configs1_literal: batches in flight in its many-in-flight leg "
+                         "(0: the default)")
+    ap.add_argument("--literal-scan-grid", type=int, default=-1,
+                    help="configs1_literal: PFSCDC_SCAN_GRID for its many-in-flight leg "
+                         "(-1: 64, as for c3)")
     ap.add_argument("--no-literal", action="store_true",
                     help="c2: skip the one-batch (unaggregated configs[1]) measurement")
     ap.add_argument("--shard", default="",

@@ -21,7 +21,7 @@ C3_BYTES = 10 * (1 << 30)
 # on one GPU: 16K chains 545 GiB/s, 21K chains 696 GiB/s, N=1's 20.5K 661; profiles/r2/scale/)
 MIN_CHAINS = 20480
 C3_INFLIGHT, C3_QUEUES, C3_SCAN_GRID = 20, 32, 64
-LITERAL_INFLIGHT = 12  # configs1_literal: batches in flight (c2 lines take C3_QUEUES queues)
+LITERAL_INFLIGHT = 20  # configs1_literal: batches in flight (c2 lines take C3_QUEUES queues)
 METRIC = "GiB/s device-resident CDC rolling-hash + chunk content-hash"
 SYNTH_DATA = "synthetic (seeded splitmix64 bytes generated in HBM)"
 

@@ -8,7 +8,7 @@ import time
 
 from . import parity as par
 from .common import (GIB, HBM_PEAK_GBS, LITERAL_INFLIGHT, METRIC, SIMDS, VALU_PEAK_GIPS,
-                     C3_INFLIGHT, fill, hit_rate, load_traffic, med, workload)
+                     C3_INFLIGHT, C3_SCAN_GRID, fill, hit_rate, load_traffic, med, workload)
 from .harness import Harness, plan_steps, steady_state
 
 
@@ -442,19 +442,29 @@ def literal_batch(args, work, chunker, data, params, local, Chunker, torch):
     # many batches in flight: LITERAL_INFLIGHT contexts (one stream and hardware queue each),
     # every call still one configs[1] batch; the batches' ~4 MiB chains overlap instead of
     # aggregating into one launch.  Steady state: 4 rounds of the contexts after one round.
-    k = LITERAL_INFLIGHT
+    from pfs_amd import _lib
+    k = args.literal_inflight if args.literal_inflight > 0 else LITERAL_INFLIGHT
+    # scans capped at C3_SCAN_GRID workgroups, as for c3's streams: a full-width scan would
+    # wait for CUs the other batches' chain-bound hashes hold (12 batches uncapped 800-873
+    # GiB/s, 20 capped 993-1,007, 24 outrun the queues: profiles/r5/literal_inflight/)
+    grid0 = _lib.get_knob("PFSCDC_SCAN_GRID")
+    _lib.set_knob("PFSCDC_SCAN_GRID", args.literal_scan_grid if args.literal_scan_grid >= 0
+                  else C3_SCAN_GRID)
     many = [chunker] + [Chunker(params, device=local) for _ in range(k - 1)]
     _alternate(many, [view] * k, offs, k)
     torch.cuda.synchronize()
     nmany = 4 * k
     piped_k = _alternate(many, [view] * k, offs, nmany) / nmany
+    grid_k = _lib.get_knob("PFSCDC_SCAN_GRID")
+    _lib.set_knob("PFSCDC_SCAN_GRID", grid0)
     for c in many[1:]:
         c.close()
     return {"value": round(sb / serial / GIB, 3), "unit": "GiB/s",
             "ms_per_batch": round(serial * 1e3, 3),
             "hash_span_ms_median": round(statistics.median(hs), 3),
             "two_in_flight_value": round(sb / piped / GIB, 3),
-            "many_in_flight": {"batches_in_flight": k, "value": round(sb / piped_k / GIB, 3),
+            "many_in_flight": {"batches_in_flight": k, "scan_grid": grid_k,
+                               "value": round(sb / piped_k / GIB, 3),
                                "ms_per_batch": round(piped_k * 1e3, 3),
                                "note": "%d contexts on %d streams, one configs[1] batch per "
                                        "call, %d batches" % (k, k, nmany)},
