@@ -242,3 +242,40 @@ print("rccl ok", len(segs))
                        timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "rccl ok" in r.stdout
+
+
+# index chunking whose min exceeds any entry here (pieces <= 200 KB of ~4 KB chunks): see
+# test_gpu_fileset.RAND_INDEX for why an entry at the index min is excluded
+RAND_INDEX = Ch.Params(average_bits=16, seed=0, min=40_000, max=400_000)
+
+
+@pytest.mark.parametrize("case", fuzz_cases(4))
+def test_commit_sharded_random_layouts_equal_single(case):
+    """Randomised commits sharded by serialized fileset over 2-6 virtual ranks: file sizes
+    (empty, exact fills, files larger than the threshold), threshold and rank count drawn per
+    case; the ranks' filesets equal one writer's, which equal the oracle's."""
+    rng = np.random.default_rng(5600 + case)
+    mem = int(rng.integers(40_000, 200_000))
+    sizes = [0 if rng.random() < 0.1 else int(rng.integers(1, int(mem * rng.choice([0.3, 1.0, 2.5]))))
+             for _ in range(int(rng.integers(5, 40)))]
+    if rng.random() < 0.5:  # an exact fill somewhere
+        k = int(rng.integers(0, len(sizes)))
+        lay = pd.commit_layout(sizes[:k + 1], mem)
+        sizes[k] += mem - int(lay.fileset_bytes()[-1])
+    world = int(rng.integers(2, 7))
+    lay = pd.commit_layout(sizes, mem)
+    st = PF.Storage(0, cp(P), mem, cp(RAND_INDEX))
+    got = []
+    for r in pd.shard_filesets(lay, world):
+        w = st.new_unordered_writer()
+        got += [(x.additive, x.deletive, x.size_bytes)
+                for x in pd.put_rank_filesets(w, lay, r, _path, _bytes)]
+    one = st.new_unordered_writer()
+    for f, n in enumerate(sizes):
+        one.put(_path(f), "", False, _bytes(f, 0, n))
+    single = [(x.additive, x.deletive, x.size_bytes) for x in one.close()]
+    assert got == single
+    ow = OF.UnorderedWriter(P, mem, RAND_INDEX)
+    for f, n in enumerate(sizes):
+        ow.put(_path(f), "", False, _bytes(f, 0, n))
+    assert single == [(x.additive, x.deletive, x.size_bytes) for x in ow.close()]
