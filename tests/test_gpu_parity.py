@@ -520,3 +520,45 @@ def test_invalid_arguments_are_refused_and_the_ctx_stays_usable():
             c.get_chunks(data, b, refs)
     assert_same(c.scan(data, offs), data, offs, SMALL)
     c.close()
+
+
+@pytest.mark.parametrize("case", fuzz_cases(1))
+def test_contexts_in_concurrent_threads_equal_oracle(case):
+    """A Go host runs many writers at once, each on its own context; here four threads each
+    own a Chunker (ctypes releases the GIL, so the library's calls run concurrently) and scan
+    random batches with different parameters, device-resident or host input.  Every result
+    equals the oracle's."""
+    import threading
+
+    import torch
+
+    params = [SMALL, Ch.Params(average_bits=14, seed=2, min=300_000, max=900_000),
+              Ch.Params(average_bits=9, seed=0, min=64, max=5000), DEFAULT]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(777 + 10 * case + t)
+            p = params[t]
+            c = Chunker(cp(p), device=0)
+            for k in range(6):
+                lens = [int(x) for x in rng.integers(0, 3 * p.max, int(rng.integers(1, 40)))]
+                offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+                data = synthetic_bytes(offs, 100_000 * case + 1000 * t + k)
+                src = torch.from_numpy(data).cuda() if k % 2 else data
+                res = c.scan(src, offs)
+                segs, begin = coracle.segment_files(data, offs, p, nthreads=2)
+                assert np.array_equal(res.file_begin, begin), (t, k)
+                for f in ("offset", "size", "file", "flags", "hash"):
+                    assert np.array_equal(res.segments[f], segs[f]), (t, k, f)
+            c.close()
+        except Exception as e:  # reported on the main thread
+            errors.append((t, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=300)
+    assert not any(th.is_alive() for th in threads), "a scan thread hung"
+    assert not errors, errors
