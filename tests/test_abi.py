@@ -288,3 +288,36 @@ def test_create_with_id_patch_applies():
     assert "return c.CreateWithID(ctx, md, Hash(chunkData), chunkData)" in create
     with_id = out[out.index("func (c *trackedClient) CreateWithID("):out.index("func (c *trackedClient) Get(")]
     assert "chunkID :=" not in with_id and "c.store.Put(ctx, key, chunkData)" in with_id
+
+
+def test_plain_c_consumer_builds_and_agrees_with_oracle(lib, tmp_path):
+    """include/pfscdc.h compiles as strict C99 (what cgo's C compiler sees) and a C program
+    linked against libpfscdc.so gets, from the host-side entry points, the oracle's table and
+    Go Int63 stream, fileset.Clean, the store's put/get/dedup and the knob table."""
+    from oracle import fileset as OF
+    exe = str(tmp_path / "abi_consumer")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "abi_consumer.c"),
+                    "-L", libdir, "-lpfscdc", "-Wl,-rpath," + libdir,
+                    "-Wl,-rpath-link,/opt/rocm/lib", "-o", exe], check=True)
+    paths = ["a//b/../c", "/", "", "x/", "./y/./z/..", "dir/sub/"]
+    seed = -7
+    res = subprocess.run([exe, str(seed)] + paths, capture_output=True, text=True, check=True)
+    lines = res.stdout.splitlines()
+    fields = {}
+    for ln in lines:
+        fields.setdefault(ln.split()[0], []).append(ln.split()[1:])
+    assert fields["params"] == [["23", "1", "1000000", "20000000"]]
+    assert [int(x, 16) for x in fields["table"][0]] == buzhash64.generate_hashes(seed)
+    src = gorand.Source(seed)
+    assert [int(x) for x in fields["int63"][0]] == [src.int63() for _ in range(8)]
+    codes = dict(re.findall(r"#define (PFSCDC_E\w+) (-\d+)", open(HEADER).read()))
+    assert fields["store"] == [["count", "1", "missing", codes["PFSCDC_ENOTFOUND"]]]
+    assert fields["ctx_null"] == [[codes["PFSCDC_EINVAL"]]]
+    assert fields["unknown_knob"] == [[codes["PFSCDC_EINVAL"]]]
+    assert [(k[0], tuple(int(x) for x in k[1:])) for k in fields["knob"]] == \
+        list(_lib.knob_info().items())
+    want = [[str(d), OF.clean(p, bool(d))] for p in paths for d in (0, 1)]
+    assert fields["clean"] == want
