@@ -321,3 +321,15 @@ def test_plain_c_consumer_builds_and_agrees_with_oracle(lib, tmp_path):
         list(_lib.knob_info().items())
     want = [[str(d), OF.clean(p, bool(d))] for p in paths for d in (0, 1)]
     assert fields["clean"] == want
+
+
+@pytest.mark.parametrize("name", ["abi_consumer", "abi_gpu_consumer", "uw_consumer"])
+def test_c_drivers_build_strict(lib, tmp_path, name):
+    """Every C driver of the ABI (tests/c/: the CPU consumer, the GPU consumer, the host-
+    sanitizer driver) compiles and links as strict C99 against the header and library."""
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", name + ".c"),
+                    "-L", libdir, "-lpfscdc", "-Wl,-rpath," + libdir,
+                    "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(tmp_path / name)], check=True)
