@@ -3,6 +3,9 @@
 # the gfx950 device code is built as usual: every -fsanitize sits behind -Xarch_host).
 #   bash tools/r5_host_sanitize.sh build   # here, on the CPU: build/asan/{libpfscdc.so,*consumer}
 #   bash tools/r5_host_sanitize.sh run OUT # on the GPU box: the C drivers under the sanitizers
+#   bash tools/r5_host_sanitize.sh build-tsan / run-tsan OUT: ThreadSanitizer over the same
+#     drivers (host code only; the UnorderedWriter's background group writers, the writer's
+#     copy threads, concurrent ctxs)
 # The drivers are plain C processes (tests/c/*.c) linked against the sanitized library, so no
 # preload is needed: the executable itself loads the shared sanitizer runtime first.
 set -euo pipefail
@@ -48,8 +51,39 @@ run)
   fi
   echo "no sanitizer reports"
   ;;
+build-tsan)
+  T=build/tsan
+  mkdir -p $T
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -pthread \
+    -fno-omit-frame-pointer -Xarch_host -fsanitize=thread -Xarch_host -shared-libsan -shared \
+    -x hip $SRC -o $T/libpfscdc.so
+  for p in abi_gpu_consumer uw_consumer; do
+    $CL -std=c99 -O1 -g -fno-omit-frame-pointer -Xarch_host -fsanitize=thread \
+      -Xarch_host -shared-libsan -Wall -Werror -Iinclude tests/c/$p.c -L$T -lpfscdc \
+      -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT -Wl,-rpath-link,/opt/rocm/lib -o $T/$p
+  done
+  ;;
+run-tsan)
+  T=build/tsan
+  OUT=${2:?output dir}
+  mkdir -p "$OUT"
+  # races inside the uninstrumented HIP/HSA runtimes are not reported; ours are
+  export TSAN_OPTIONS="halt_on_error=0:exitcode=26:report_signal_unsafe=0:history_size=4"
+  timeout -k 10 200 $T/abi_gpu_consumer "$OUT/data.bin" 12 1 2000 30000 50000 \
+    0 1 63 64 65 1999 2000 2001 29999 30000 30001 100000 250000 7 0 40000 \
+    > "$OUT/abi_gpu_consumer.out" 2> "$OUT/abi_gpu_consumer.err"
+  echo "abi_gpu_consumer ok"
+  rm -f "$OUT/data.bin"
+  timeout -k 10 300 $T/uw_consumer 400 7 > "$OUT/uw_consumer.out" 2> "$OUT/uw_consumer.err"
+  grep -q '^done$' "$OUT/uw_consumer.out"
+  echo "uw_consumer ok"
+  if grep -l "WARNING: ThreadSanitizer" "$OUT"/*.err; then
+    exit 27
+  fi
+  echo "no ThreadSanitizer reports"
+  ;;
 *)
-  echo "usage: $0 build | run OUT" >&2
+  echo "usage: $0 build | run OUT | build-tsan | run-tsan OUT" >&2
   exit 2
   ;;
 esac
