@@ -67,16 +67,24 @@ run-tsan)
   T=build/tsan
   OUT=${2:?output dir}
   mkdir -p "$OUT"
-  # races inside the uninstrumented HIP/HSA runtimes are not reported; ours are
-  export TSAN_OPTIONS="halt_on_error=0:exitcode=26:report_signal_unsafe=0:history_size=4"
+  # The HIP/HSA runtimes are not instrumented: their threads synchronize through HSA signals
+  # TSan cannot see, so their own malloc/free (interceptors called from those libraries) read
+  # as races (profiles/r5/sanitize/tsan_unsuppressed_head.txt).  Those calls are ignored; every
+  # access made by this library's code is still checked.
+  printf 'called_from_lib:libhsa-runtime64.so.1\ncalled_from_lib:libamdhip64.so.7\ncalled_from_lib:libhsakmt.so.1\n' > "$OUT/tsan.supp"
+  export TSAN_OPTIONS="halt_on_error=0:exitcode=26:report_signal_unsafe=0:history_size=4:suppressions=$OUT/tsan.supp:print_suppressions=1"
+  rc=0
   timeout -k 10 200 $T/abi_gpu_consumer "$OUT/data.bin" 12 1 2000 30000 50000 \
     0 1 63 64 65 1999 2000 2001 29999 30000 30001 100000 250000 7 0 40000 \
-    > "$OUT/abi_gpu_consumer.out" 2> "$OUT/abi_gpu_consumer.err"
-  echo "abi_gpu_consumer ok"
+    > "$OUT/abi_gpu_consumer.out" 2> "$OUT/abi_gpu_consumer.err" || rc=$?
+  echo "abi_gpu_consumer rc=$rc"
   rm -f "$OUT/data.bin"
-  timeout -k 10 300 $T/uw_consumer 400 7 > "$OUT/uw_consumer.out" 2> "$OUT/uw_consumer.err"
+  [ $rc -eq 0 ] || [ $rc -eq 26 ] || exit $rc
+  rc=0
+  timeout -k 10 300 $T/uw_consumer 400 7 > "$OUT/uw_consumer.out" 2> "$OUT/uw_consumer.err" || rc=$?
+  echo "uw_consumer rc=$rc"
+  [ $rc -eq 0 ] || [ $rc -eq 26 ] || exit $rc
   grep -q '^done$' "$OUT/uw_consumer.out"
-  echo "uw_consumer ok"
   if grep -l "WARNING: ThreadSanitizer" "$OUT"/*.err; then
     exit 27
   fi
