@@ -1,10 +1,11 @@
 /* A plain C99 driver of the host-heavy entry points, for the host-sanitizer run
  * (tools/r5_host_sanitize.sh): the UnorderedWriter (Put, append, Delete, directory deletes,
  * grouped background fileset writes), the chunk store, Writer.Copy of another writer's
- * DataRefs and MergeFileReader.Hash.  Parity of these paths is tested from Python against the
+ * DataRefs, MergeFileReader.Hash, and four threads scanning at once, each on its own ctx.  Parity of these paths is tested from Python against the
  * oracle; this program only has to drive them through a sanitized library and print a
  * summary.  usage: uw_consumer NFILES SEED */
 #include <inttypes.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -72,6 +73,37 @@ static int on_chunk(void* user, const pfscdc_chunk_ref* c, const pfscdc_annotati
     nrefs++;
   }
   return 0;
+}
+
+/* distinct ctxs may run concurrently (pfscdc.h): each thread scans the same batch twice */
+typedef struct {
+  const uint8_t* data;
+  const uint64_t* offs;
+  uint32_t nfiles;
+  uint64_t nsegs;
+  uint8_t digest0[32];
+  int rc;
+} scan_job;
+
+static void* scan_thread(void* arg) {
+  scan_job* j = (scan_job*)arg;
+  pfscdc_params p;
+  pfscdc_ctx* c = NULL;
+  int r;
+  pfscdc_default_params(&p);
+  p.average_bits = 12;
+  p.min_chunk = 2000;
+  p.max_chunk = 30000;
+  j->rc = pfscdc_ctx_create(&p, 0, &c);
+  for (r = 0; r < 2 && j->rc == PFSCDC_OK; r++) {
+    j->rc = pfscdc_scan(c, j->data, j->offs[j->nfiles], 0, j->offs, j->nfiles);
+    if (j->rc == PFSCDC_OK) {
+      j->nsegs = pfscdc_num_segments(c);
+      if (j->nsegs) memcpy(j->digest0, pfscdc_segments(c)[0].hash, 32);
+    }
+  }
+  if (c) pfscdc_ctx_destroy(c);
+  return NULL;
 }
 
 int main(int argc, char** argv) {
@@ -166,6 +198,32 @@ int main(int argc, char** argv) {
     printf("\n");
   }
   OK(pfscdc_store_destroy(store), NULL);
+
+  /* 4. four threads, four ctxs, the same batch */
+  {
+    pthread_t th[4];
+    scan_job jobs[4];
+    uint64_t* offs = (uint64_t*)calloc(nfiles + 1, sizeof *offs);
+    if (!offs) return 1;
+    for (f = 0; f < nfiles; f++) offs[f + 1] = offs[f] + lens[f];
+    for (i = 0; i < 4; i++) {
+      memset(&jobs[i], 0, sizeof jobs[i]);
+      jobs[i].data = data;
+      jobs[i].offs = offs;
+      jobs[i].nfiles = nfiles;
+      if (pthread_create(&th[i], NULL, scan_thread, &jobs[i]) != 0) return 1;
+    }
+    for (i = 0; i < 4; i++) pthread_join(th[i], NULL);
+    for (i = 0; i < 4; i++) {
+      if (jobs[i].rc != PFSCDC_OK || jobs[i].nsegs != jobs[0].nsegs ||
+          memcmp(jobs[i].digest0, jobs[0].digest0, 32) != 0) {
+        fprintf(stderr, "thread %u: rc %d, %" PRIu64 " segments\n", i, jobs[i].rc, jobs[i].nsegs);
+        return 1;
+      }
+    }
+    printf("threads 4 segments %" PRIu64 "\n", jobs[0].nsegs);
+    free(offs);
+  }
   {
     uint64_t freed = 0;
     uint32_t ctxs = 0;
