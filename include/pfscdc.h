@@ -486,8 +486,14 @@ int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t ca
  * non-numeric or out-of-range variable leaves the default (a bad value is reported on stderr).
  * No knob changes any result: they select between exact forms of the same computation or size
  * the host-fed writer's pools.  pfscdc_set_knob changes a knob for the whole process (atomic:
- * a launch already enqueued keeps the value it read; the host-fed writer reads its knobs when
- * it is created).  PFSCDC_EINVAL for an unknown name or a value outside the knob's range. */
+ * a launch already enqueued keeps the value it read).  When a knob takes effect:
+ *   PFSCDC_UW_* (and PFSCDC_CTX_CACHE for the contexts it makes): when an unordered writer
+ *     is created, for that writer's lifetime;
+ *   PFSCDC_COPY_THREADS: once, when the first large Put builds the process-wide copy pool;
+ *     from then on setting it to another value returns PFSCDC_ESTATE;
+ *   every other knob: at the next call that launches the kernels it selects.
+ * PFSCDC_EINVAL for an unknown name or a value outside the knob's range.  A PFSCDC_* variable
+ * in the environment that is not a knob is reported on stderr and ignored. */
 int pfscdc_set_knob(const char* name, int64_t value);
 int pfscdc_get_knob(const char* name, int64_t* value);
 /* The i-th knob's name (0-based), NULL past the last; lo/hi (nullable) its range and def

@@ -309,9 +309,20 @@ class knobs:
         self.old = {}
 
     def __enter__(self):
-        for k, v in self.kv.items():
-            self.old[k] = get_knob(k)
-            set_knob(k, v)
+        info = knob_info()
+        for k, v in self.kv.items():  # every name and range first: all or nothing
+            if k not in info:
+                raise PfsCdcError(PFSCDC_EINVAL, f"unknown knob {k}")
+            lo, hi, _ = info[k]
+            if not lo <= int(v) <= hi:
+                raise PfsCdcError(PFSCDC_EINVAL, f"knob {k}={v} outside [{lo}, {hi}]")
+        try:
+            for k, v in self.kv.items():
+                self.old[k] = get_knob(k)
+                set_knob(k, v)
+        except BaseException:
+            self.__exit__()
+            raise
         return self
 
     def __exit__(self, *exc):

@@ -35,16 +35,6 @@
 
 #define PFS_DEV __device__ __forceinline__
 
-// Timing-only knobs (tools/ab_*.sh A/B builds) that drop the table lookup, the rotation, the
-// LDS address permute or the DMA wait: they produce wrong cuts and digests, so a build that
-// defines one must also say so explicitly; the product Makefile never does.
-#if defined(PFS_EXP_NO_TABLE) || defined(PFS_EXP_NO_ROT) || defined(PFS_EXP_NO_PERM) || \
-    defined(PFS_EXP_NO_DMA_WAIT) || defined(PFS_EXP_MSG_SAME)
-#ifndef PFS_TIMING_ONLY_BUILD
-#error "PFS_EXP_NO_* knobs give wrong results: define PFS_TIMING_ONLY_BUILD for a timing-only build"
-#endif
-#endif
-
 namespace pfscdc {
 
 // ------------------------------------------------------------------------------------------
@@ -55,11 +45,7 @@ PFS_DEV uint64_t rotl1_64(uint64_t x) { return (x << 1) | (x >> 63); }
 
 // LDS byte address of T[byte j of w] in this lane's copy: (idx << 8) | (lane & 31) * 8.
 PFS_DEV uint32_t tab_addr(uint32_t w, uint32_t lane_off, int j) {
-#ifdef PFS_EXP_NO_PERM
-  return __builtin_amdgcn_bitop3_b32(w, 0xFF00u, lane_off, 0xEC);  // (w & m) | l (timing only)
-#else
   return __builtin_amdgcn_perm(w, lane_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
-#endif
 }
 
 template <typename T>
@@ -210,26 +196,15 @@ struct StaticFor {
 // lgkmcnt(0) around LDS-DMA); consumers sit behind an explicit s_waitcnt + sched_barrier.
 PFS_DEV uint64_t lds_read_async(uint32_t a) {
   uint64_t v;
-#ifdef PFS_EXP_NO_TABLE
-  v = ((uint64_t)(a ^ 0x7F4A7C15u) << 32) | (a ^ 0xC2B2AE35u);
-#else
   asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
-#endif
   return v;
 }
 
-#ifndef PFS_EXP_AHEAD
-#define PFS_EXP_AHEAD 6
-#endif
-static_assert(PFS_EXP_AHEAD >= 1 && 2 * (PFS_EXP_AHEAD - 1) <= 15, "lgkmcnt is 4 bits");
-constexpr int kRollAhead = PFS_EXP_AHEAD;
-#ifdef PFS_EXP_NO_ROT
-#define PFS_ROT1(NL, NH) const uint32_t NL = hh, NH = hl;  /* timing only */
-#else
+constexpr int kRollAhead = 6;  // bytes of T lookups in flight (2 ds_read_b64 each)
+static_assert(kRollAhead >= 1 && 2 * (kRollAhead - 1) <= 15, "lgkmcnt is 4 bits");
 #define PFS_ROT1(NL, NH)                                   \
   const uint32_t NL = __builtin_amdgcn_alignbit(hl, hh, 31); \
   const uint32_t NH = __builtin_amdgcn_alignbit(hh, hl, 31);
-#endif  // bytes of T lookups in flight (2 ds_read_b64 each; lgkmcnt <= 15)
 
 // Roll 64 positions: IN = this block's 16 dwords, OUT = the block 64 bytes earlier; test all
 // 64 positions with one min-reduce and fall into the exact re-roll only if one hit.
@@ -295,19 +270,9 @@ PFS_DEV void record_block_g(const uint8_t* __restrict__ data, const uint8_t* __r
   record_block(data, tail, n_main, h, pos, n, tile_base, mask64, table, rec, plan);
 }
 
-#ifndef PFS_SCAN_DYN
-#define PFS_SCAN_DYN 1  // scan work units from a counter (1) or round-robin tiles (0)
-#endif
-
-#ifndef PFS_EXP_GAHEAD
-#define PFS_EXP_GAHEAD 10
-#endif
-static_assert(PFS_EXP_GAHEAD >= 1 && PFS_EXP_GAHEAD - 1 <= 15, "lgkmcnt is 4 bits");
-constexpr int kGAhead = PFS_EXP_GAHEAD;  // T[in] lookups in flight (one ds_read_b64 each)
-#ifndef PFS_EXP_GWAIT
-#define PFS_EXP_GWAIT 2
-#endif
-constexpr int kGWait = PFS_EXP_GWAIT;  // positions per s_waitcnt
+constexpr int kGAhead = 10;  // T[in] lookups in flight (one ds_read_b64 each)
+static_assert(kGAhead >= 1 && kGAhead - 1 <= 15, "lgkmcnt is 4 bits");
+constexpr int kGWait = 2;  // positions per s_waitcnt
 static_assert(64 % kGWait == 0 && kGWait <= kGAhead, "wait groups tile the block");
 
 #define PFS_ROLL64G(IN, POS)                                                              \
@@ -496,7 +461,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
   const uint32_t swz_l = stage_swz(lane);
   __syncthreads();  // table copies written; from here on every wave runs on its own
 
-#if PFS_SCAN_DYN
   // Work unit = one wave's 64 strips of a tile.  Each wave takes the next unit from a
   // launch-wide counter (zeroed before the launch), so CUs that start late (another step's
   // hash still draining there) simply take fewer units instead of finishing last.
@@ -515,11 +479,6 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
     if (plan) scan_unit_plan(plan, slot, lane, n, unit, skip, fr);
     const uint64_t tile = unit / kScanWaves;
     const uint64_t wslot = unit % kScanWaves;
-#else
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t wslot = wave;
-    uint32_t skip = 0;
-#endif
     TileRec* const rec = recs + tile;
     const uint64_t tile_base = tile * kTile;
     // Leading 128-byte steps of this unit's strips that hold no eligible position (inside
@@ -589,9 +548,7 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
       const uint32_t cand_thr = 1u << kshift;
       const bool active = s0 < n;
       for (uint32_t step = 0; step < nsteps; step++) {
-#ifndef PFS_EXP_NO_DMA_WAIT
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's DMA has landed
-#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int c = 0; c < 8; c++) {
@@ -622,10 +579,8 @@ __global__ __launch_bounds__(kScanBlock) __attribute__((amdgpu_waves_per_eu(kSca
         }
       }
     }
-#if PFS_SCAN_DYN
     if (lane == 0) u0 = atomicAdd(unit_ctr, 1u);  // the next unit, in flight during the report
     if (fr != ~0u) scan_unit_report(plan, fr, lane);
-#endif
   }
   // the last workgroup compacts the tile records into the sorted entry list (the table and
   // staging LDS are free once every wave of the workgroup is past its last unit)
@@ -1487,11 +1442,6 @@ PFS_DEV void fold_diag(uint64_t& ha, uint64_t& hb, uint64_t a, uint64_t b, uint6
 }
 
 constexpr int kModeHash = 0, kModeRefId = 1, kModeGet = 2;
-// Development trace (PFSCDC_WAVE_TRACE, timing only): per hash wave its end time and its
-// hardware slot (HW_ID, XCC_ID), to read how the launch drains.  nullptr: off.
-#ifdef PFS_WAVE_TRACE
-__device__ uint64_t* g_wave_trace = nullptr;
-#endif
 template <int MODE>
 __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void blake2b_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
@@ -1633,34 +1583,20 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
         pre[2] = lds_abs_u64(ma[0][2] + nxt);
         pre[3] = lds_abs_u64(ma[0][3] + nxt);
       }
-#ifdef PFS_HASH_CXX
-      if (r == 0) d ^= dt;
-      PFS_G(a, b, c, d, x0, x1);           // column step: G_j on (v[j], v[4+j], v[8+j], v[12+j])
-      a = quad_perm64<0x93>(a);            // a <- v[(j+3)%4]
-      c = quad_perm64<0x39>(c);            // c <- v[8+(j+1)%4]
-      d = quad_perm64<0x4E>(d);            // d <- v[12+(j+2)%4]
-      PFS_G(a, b, c, d, x2, x3);           // diagonal step through b_j: G_{4+(j+3)%4}
-      a = quad_perm64<0x39>(a);
-      c = quad_perm64<0x93>(c);
-      d = quad_perm64<0x4E>(d);
-#else
       if (r == 0) {  // leaves a, c, d in the diagonal layout
         const uint64_t a0 = a, b0 = b, c0 = c, d0 = d;
         PFS_ROUND_FIRST(a0, b0, c0, d0, dt, x0, x1, x2, x3);
       } else {
         PFS_ROUND(false, x0, x1, x2, x3);
       }
-#endif
       x0 = y0; x1 = y1; x2 = y2; x3 = y3;
       if (r == 5) put_next();
     }
-#ifndef PFS_HASH_CXX
     if (back) {
       a = quad_perm64<0x39>(a);  // back to the column layout
       c = quad_perm64<0x93>(c);
       d = quad_perm64<0x4E>(d);
     }
-#endif
   };
 
   // A block in a run of quiet blocks (content hash only): every active quad is at least 4
@@ -1685,11 +1621,7 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
     rounds(par, a, b, c, d, [&] {
       if (active) {
         lds_put(nxt);
-#ifdef PFS_EXP_MSG_SAME  // timing only: every fast block loads the segment's first block (L2)
-        msg_load_full(m0, m1, src + 32 * j);
-#else
         msg_load_full(m0, m1, src + (blk + 2) * 128 + 32 * j);
-#endif
       }
     }, pre, false, tm);
     fold_diag(ha, hb, a, b, c, d);
@@ -1875,29 +1807,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1, 2
       }
     }
   }
-#ifdef PFS_WAVE_TRACE
-  if (MODE == kModeHash && g_wave_trace && lane == 0) {
-    const uint64_t w = (uint64_t)blockIdx.x * (kHashBlock / 64) + (threadIdx.x >> 6);
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // HW_REG_XCC_ID
-    g_wave_trace[4 * w] = __builtin_amdgcn_s_memrealtime();
-    g_wave_trace[4 * w + 1] = (uint64_t)hw | ((uint64_t)xcc << 32);
-    g_wave_trace[4 * w + 2] = wave_steps;
-    g_wave_trace[4 * w + 3] = __builtin_amdgcn_s_memtime() - span_clk.t0;  // shader cycles
-  }
-#endif
   span_end(span, span_clk);
 }
-
-#ifdef PFS_WAVE_TRACE
-hipError_t set_wave_trace(uint64_t* p, hipStream_t st) {
-  // stream-ordered and synchronous w.r.t. the host value (a development tool: the copy
-  // source must outlive the call)
-  hipError_t e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return e;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_trace), &p, sizeof p, 0, hipMemcpyHostToDevice);
-}
-#endif
 
 // 5d. ChaCha20 ciphertext of whole chunks, one lane per 64-byte keystream block (the Ref.Id
 // pass split in two for chunk lists that cannot fill the GPU, see create_refs_device).  Every
@@ -2074,139 +1985,6 @@ PFS_DEV void b2_compress_lane(uint64_t (&h)[8], const uint64_t (&x)[16], uint64_
 #pragma unroll
   for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
 }
-
-#if PFS_HASH_LANES == 1  // the one-lane-per-segment form (compile-time A/B only)
-// One 128-byte block for this lane: eight 16-byte loads.
-PFS_DEV void blk_load_full(uint4 (&m)[8], const uint8_t* p) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) __builtin_memcpy(&m[i], p + 16 * i, 16);
-}
-
-// Last block of a segment: bytes at or past `avail` zeroed (see msg_load_tail).
-PFS_DEV void blk_load_tail(uint4 (&m)[8], const uint8_t* p, int64_t avail, const uint8_t* end) {
-  if (p + 128 <= end) {
-    blk_load_full(m, p);
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      m[i].x &= keep_bytes(avail - 16 * i - 0);
-      m[i].y &= keep_bytes(avail - 16 * i - 4);
-      m[i].z &= keep_bytes(avail - 16 * i - 8);
-      m[i].w &= keep_bytes(avail - 16 * i - 12);
-    }
-    return;
-  }
-  uint32_t w[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) {
-    uint32_t v = 0;
-    for (int b = 0; b < 4; b++)
-      if (4 * i + b < avail) v |= (uint32_t)p[4 * i + b] << (8 * b);
-    w[i] = v;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) m[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-}
-
-// Block `b` (0-based) of a segment of L bytes into m.
-PFS_DEV void blk_load(uint4 (&m)[8], const uint8_t* src, uint64_t b, uint64_t L, uint64_t nblk,
-                      const uint8_t* end) {
-  const uint8_t* p = src + b * 128;
-  if (b + 1 == nblk) blk_load_tail(m, p, (int64_t)(L - b * 128), end);
-  else blk_load_full(m, p);
-}
-
-__global__ __launch_bounds__(kHashLaneBlock) void blake2b_lane_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs,
-    pfscdc_segment* __restrict__ segs, const uint64_t* __restrict__ seg_count,
-    const uint32_t* __restrict__ order, uint32_t* __restrict__ counter, uint64_t nbytes) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nseg = *seg_count;
-  const uint8_t* const end = data + nbytes;
-  bool active = false;   // this lane holds a segment
-  bool drained = false;  // wave-uniform: the queue is exhausted
-  uint64_t L = 0, nblk = 0, blk = 0;
-  const uint8_t* src = data;
-  pfscdc_segment* seg = segs;
-  uint64_t h[8];
-  uint4 m[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    h[i] = 0;
-    m[i] = make_uint4(0, 0, 0, 0);
-  }
-
-  while (true) {
-    if (!drained) {
-      const bool need = !active;
-      const uint64_t want = __ballot(need);
-      if (want) {
-        const uint32_t cnt = (uint32_t)__popcll(want);
-        const uint32_t leader = (uint32_t)__builtin_ctzll(want);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(counter, cnt);
-        base = (uint32_t)__shfl((int)base, (int)leader, 64);
-        if (need) {
-          const uint64_t idx = (uint64_t)base + (uint64_t)__popcll(want & ((1ULL << lane) - 1));
-          if (idx < nseg) {
-            seg = segs + order[idx];
-            L = seg->size;
-            src = data + offs[seg->file] + seg->offset;
-            nblk = L == 0 ? 1 : (L + 127) / 128;
-            blk = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) h[i] = kIV[i];
-            h[0] ^= 0x01010020ULL;  // digest 32 bytes, fanout 1, depth 1
-            active = true;
-            blk_load(m, src, 0, L, nblk, end);
-          }
-        }
-        if ((uint64_t)base + cnt >= nseg) drained = true;
-      }
-    }
-    if (__ballot(active) == 0) break;  // every lane idle and the queue empty
-
-    const bool last = blk + 1 == nblk;
-    uint64_t x[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      x[2 * i] = mk64(m[i].x, m[i].y);
-      x[2 * i + 1] = mk64(m[i].z, m[i].w);
-    }
-    if (active && !last) blk_load(m, src, blk + 1, L, nblk, end);  // prefetch the next block
-    const uint64_t t = last ? L : (blk + 1) * 128;
-    uint64_t v[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      v[i] = h[i];
-      v[8 + i] = kIV[i];
-    }
-    v[12] ^= t;
-    v[14] ^= last ? ~0ULL : 0ULL;
-#pragma unroll
-    for (int r = 0; r < 12; r++) {
-      PFS_G(v[0], v[4], v[8], v[12], x[kSigma[r][0]], x[kSigma[r][1]]);
-      PFS_G(v[1], v[5], v[9], v[13], x[kSigma[r][2]], x[kSigma[r][3]]);
-      PFS_G(v[2], v[6], v[10], v[14], x[kSigma[r][4]], x[kSigma[r][5]]);
-      PFS_G(v[3], v[7], v[11], v[15], x[kSigma[r][6]], x[kSigma[r][7]]);
-      PFS_G(v[0], v[5], v[10], v[15], x[kSigma[r][8]], x[kSigma[r][9]]);
-      PFS_G(v[1], v[6], v[11], v[12], x[kSigma[r][10]], x[kSigma[r][11]]);
-      PFS_G(v[2], v[7], v[8], v[13], x[kSigma[r][12]], x[kSigma[r][13]]);
-      PFS_G(v[3], v[4], v[9], v[14], x[kSigma[r][14]], x[kSigma[r][15]]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
-    if (active) {
-      blk++;
-      if (last) {  // digest = h[0..3] little endian
-        uint4* out = reinterpret_cast<uint4*>(seg->hash);
-        out[0] = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
-        out[1] = make_uint4((uint32_t)h[2], (uint32_t)(h[2] >> 32), (uint32_t)h[3], (uint32_t)(h[3] >> 32));
-        active = false;
-      }
-    }
-  }
-}
-#endif
 
 // ------------------------------------------------------------------------------------------
 // synthetic data (bench/tests): splitmix64 finalizer of (file << 40 | word) + gamma*(seed+1)
@@ -2406,17 +2184,6 @@ hipError_t launch_blake2b(const uint8_t* data, const uint64_t* offs, pfscdc_segm
                           uint32_t fair_every) {
   if (max_segments == 0) return hipSuccess;
   if (!ordered) hash_order_kernel<<<1, kCompactBlock, 0, st>>>(segs, seg_count, order, counter);
-#if PFS_HASH_LANES == 1
-  if (kHashLanesPerSegment == 1) {
-    const uint64_t need = (max_segments + kHashLaneBlock - 1) / kHashLaneBlock;
-    const uint64_t full = (uint64_t)num_cus * 4 * (waves > 0 ? waves : kHashWavesPerSimd) /
-                          (kHashLaneBlock / 64);
-    const uint64_t grid = need < full ? need : full;
-    blake2b_lane_kernel<<<(unsigned)grid, kHashLaneBlock, 0, st>>>(data, offs, segs, seg_count,
-                                                                   order, counter, nbytes);
-    return hipGetLastError();
-  }
-#endif
   // cu_exclusive: 64 KiB of unused dynamic LDS on top of the 20 KiB message buffers, so no
   // two workgroups (of this or of another launch) share a CU.  A chain-bound launch at one
   // wave per SIMD has one workgroup per CU anyway; the reservation keeps a second such launch

@@ -638,7 +638,7 @@ class CopyPool {
   CopyPool() {
     const unsigned hw = std::thread::hardware_concurrency();
     unsigned t = std::min(16u, hw ? hw : 1u);
-    if (const int64_t k = pfscdc::knob(pfscdc::Knob::CopyThreads)) t = (unsigned)k;
+    if (const int64_t k = pfscdc::knob_freeze(pfscdc::Knob::CopyThreads)) t = (unsigned)k;
     for (unsigned i = 1; i < t; i++) workers_.emplace_back([this] { run(); });
     for (auto& w : workers_) w.detach();
   }

@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <unistd.h>  // environ
+
 #include "pfscdc_internal.h"
 
 namespace pfscdc {
@@ -49,7 +51,9 @@ static_assert(kDefs[(int)Knob::kCount - 1].name != nullptr, "one entry per Knob"
 
 struct Table {
   std::atomic<int64_t> v[(int)Knob::kCount];
+  std::atomic<bool> frozen[(int)Knob::kCount];  // read once by a process-wide pool, now fixed
   Table() {
+    for (auto& f : frozen) f.store(false, std::memory_order_relaxed);
     for (int i = 0; i < (int)Knob::kCount; i++) {
       const KnobDef& d = kDefs[i];
       int64_t x = d.def;
@@ -65,6 +69,19 @@ struct Table {
           x = y;
       }
       v[i].store(x, std::memory_order_relaxed);
+    }
+    // a PFSCDC_* variable the table does not hold (a misspelling, or the knob of a removed
+    // form) would otherwise be ignored without a word
+    for (char** e = environ; e && *e; e++) {
+      if (std::strncmp(*e, "PFSCDC_", 7) != 0) continue;
+      const char* eq = std::strchr(*e, '=');
+      const size_t len = eq ? (size_t)(eq - *e) : std::strlen(*e);
+      bool known = false;
+      for (int i = 0; i < (int)Knob::kCount && !known; i++)
+        known = std::strlen(kDefs[i].name) == len && std::strncmp(kDefs[i].name, *e, len) == 0;
+      if (!known)
+        std::fprintf(stderr, "pfscdc: ignoring %.*s (not a knob of this library; "
+                     "INTEGRATION.md lists them)\n", (int)len, *e);
     }
   }
 };
@@ -85,6 +102,11 @@ int find(const char* name) {
 
 int64_t knob(Knob k) { return table().v[(int)k].load(std::memory_order_relaxed); }
 
+int64_t knob_freeze(Knob k) {
+  table().frozen[(int)k].store(true, std::memory_order_relaxed);
+  return knob(k);
+}
+
 }  // namespace pfscdc
 
 extern "C" {
@@ -94,7 +116,12 @@ int pfscdc_set_knob(const char* name, int64_t value) {
   if (i < 0) return PFSCDC_EINVAL;
   const pfscdc::KnobDef& d = pfscdc::kDefs[i];
   if (value < d.lo || value > d.hi) return PFSCDC_EINVAL;
-  pfscdc::table().v[i].store(value, std::memory_order_relaxed);
+  auto& t = pfscdc::table();
+  // a knob a process-wide pool has already read (PFSCDC_COPY_THREADS) can no longer change
+  if (t.frozen[i].load(std::memory_order_relaxed) &&
+      value != t.v[i].load(std::memory_order_relaxed))
+    return PFSCDC_ESTATE;
+  t.v[i].store(value, std::memory_order_relaxed);
   return PFSCDC_OK;
 }
 

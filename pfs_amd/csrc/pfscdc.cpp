@@ -93,9 +93,6 @@ struct pfscdc_ctx {
   DevBuf<uint4> d_uslots;
   DevBuf<uint32_t> d_rslots;
   DevBuf<ScanPlan> d_planhdr;  // the scan kernel's view of the plan (scan_slots_kernel stores it)
-#ifdef PFS_WAVE_TRACE
-  DevBuf<uint64_t> d_wtrace;    // development builds: per hash wave end time + hardware slot
-#endif
   bool scan_skipped = false;    // the last scan ran with d_skip (d_counts[3] = bytes scanned,
                                 // less d_counts[6] the settled cuts removed)
   uint32_t scan_mode = 0;       // the last scan's PFSCDC_SCAN_SKIPPED_* bits
@@ -562,14 +559,6 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
   // enqueued hash (the scans still overlap the hash tails; two hashes never share the CUs)
   if (c->hash_after && c->hash_after->device == c->device)
     HIP_OK(c, hipStreamWaitEvent(st, c->hash_after->ev[4], 0));
-#ifdef PFS_WAVE_TRACE
-  const char* wtrace = getenv("PFS_WAVE_TRACE_FILE");  // development builds only
-  if (wtrace) {
-    HIP_OK(c, c->d_wtrace.ensure(1 << 17));
-    HIP_OK(c, hipMemsetAsync(c->d_wtrace.p, 0, sizeof(uint64_t) << 17, st));
-    HIP_OK(c, set_wave_trace(c->d_wtrace.p, st));
-  }
-#endif
   // a chain-bound launch (one wave per SIMD) keeps its CUs to itself (launch_blake2b); with
   // hash bins the waves of a SIMD share the issue fairly (the PFSCDC_HASH_FAIR knob)
   if (nfiles && !(options & kScanNoHash))
@@ -579,9 +568,6 @@ int scan_async_impl(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes
                              knob(Knob::HashFair) && waves > 1 && next ? c->d_counts.p + 5
                                                                       : nullptr,
                              (uint32_t)knob(Knob::HashFairEvery)));
-#ifdef PFS_WAVE_TRACE
-  if (wtrace) HIP_OK(c, set_wave_trace(nullptr, st));
-#endif
   HIP_OK(c, hipEventRecord(c->ev[4], st));
   c->have_refs = (options & PFSCDC_OPT_REF_IDS) != 0 && !(options & kScanNoHash);
   if (c->have_refs && nfiles)
@@ -644,19 +630,6 @@ int pfscdc_wait(pfscdc_ctx* c) {
   c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] - c->h_span.p[kSpanSlots + 3] : c->nbytes;
   c->nsegs = total;
   c->scan_valid = true;
-#ifdef PFS_WAVE_TRACE
-  if (const char* wtrace = getenv("PFS_WAVE_TRACE_FILE")) {  // development trace: append
-    std::vector<uint64_t> t(1 << 17);
-    HIP_OK(c, hipMemcpy(t.data(), c->d_wtrace.p, sizeof(uint64_t) << 17, hipMemcpyDeviceToHost));
-    uint64_t sp[4];
-    HIP_OK(c, hipMemcpy(sp, c->d_span.p, sizeof sp, hipMemcpyDeviceToHost));
-    if (FILE* f = fopen(wtrace, "ab")) {
-      fwrite(sp, sizeof sp, 1, f);
-      fwrite(t.data(), sizeof(uint64_t), t.size(), f);
-      fclose(f);
-    }
-  }
-#endif
   return PFSCDC_OK;
 }
 

@@ -10,15 +10,9 @@ namespace pfscdc {
 // candidate scan geometry: waves x 64 lanes x 4 KiB strips per tile.  Candidates go
 // straight to the tile's record in global memory (zeroed before the scan), so waves never
 // synchronise per tile and all LDS beyond the table is staging.
-#ifndef PFS_SCAN_WAVES
-#define PFS_SCAN_WAVES 12
-#endif
-constexpr int kScanWaves = PFS_SCAN_WAVES;  // 12 = 3 per SIMD: LDS exactly full (8: 2 per SIMD, 3.5% slower)
+constexpr int kScanWaves = 12;  // 12 = 3 per SIMD: LDS exactly full (8: 2 per SIMD, 3.5% slower)
 constexpr int kScanBlock = 64 * kScanWaves;
-#ifndef PFS_SCAN_STRIP
-#define PFS_SCAN_STRIP 4096
-#endif
-constexpr int kStrip = PFS_SCAN_STRIP;  // bytes per lane per tile (plus a 64-byte halo)
+constexpr int kStrip = 4096;  // bytes per lane per tile (plus a 64-byte halo)
 constexpr uint64_t kTile = (uint64_t)kScanBlock * kStrip;
 constexpr int kTileK = 15;          // candidates kept per tile before it is marked dense
 constexpr uint32_t kTableLdsBytes = 256u * 256u;  // T x 32 bank-disjoint copies
@@ -29,15 +23,7 @@ constexpr int kCompactBlock = 1024;
 constexpr int kSelectBlock = 1024;  // 16 files (waves) per block; the last block's tail (segment
                                     // compaction, LPT order) runs on all 1024 threads
 constexpr int kHashBlock = 256;     // 64 quads (one segment each at a time) per block
-#ifndef PFS_HASH_WAVES_PER_SIMD
-#define PFS_HASH_WAVES_PER_SIMD 2
-#endif
-constexpr int kHashWavesPerSimd = PFS_HASH_WAVES_PER_SIMD;  // 2 saturate VALU issue (SIMD-32)
-#ifndef PFS_HASH_LANES
-#define PFS_HASH_LANES 4
-#endif
-constexpr int kHashLanesPerSegment = PFS_HASH_LANES;  // 4: blake2b_kernel (product), 1: blake2b_lane_kernel (A/B)
-constexpr int kHashLaneBlock = 256;
+constexpr int kHashWavesPerSimd = 2;  // 2 saturate VALU issue (SIMD-32)
 constexpr uint64_t kDenseBit = 1ULL << 63;
 constexpr uint64_t kNone = ~0ULL;
 constexpr uint32_t kNoNext = 0xffffffffu;  // hash bins: no following segment
@@ -61,6 +47,8 @@ enum class Knob : int {
   kCount
 };
 int64_t knob(Knob k);
+// the knob's value, fixed from now on (pfscdc_set_knob to another value: PFSCDC_ESTATE)
+int64_t knob_freeze(Knob k);
 
 void generate_hashes(int64_t seed, uint64_t out[256]);
 const pfscdc_params& ctx_params(const pfscdc_ctx* ctx);
@@ -109,9 +97,6 @@ bool ctx_scan_valid(const pfscdc_ctx* ctx);
 uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
 uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
 
-#ifdef PFS_WAVE_TRACE
-hipError_t set_wave_trace(uint64_t* p, hipStream_t st);  // development builds: per-wave trace
-#endif
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 
 // Scan work unit = one wave's 64 strips of a tile; kUnitSteps 128-byte strip steps of
