@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -pthread
-SRC := pfs_amd/csrc/cdc_kernels.hip pfs_amd/csrc/pfscdc.cpp pfs_amd/csrc/writer.cpp pfs_amd/csrc/fileset.cpp pfs_amd/csrc/gorand.cpp pfs_amd/csrc/knobs.cpp
+SRC := pfs_amd/csrc/cdc_kernels.hip pfs_amd/csrc/pfscdc.cpp pfs_amd/csrc/writer.cpp pfs_amd/csrc/fileset.cpp pfs_amd/csrc/group.cpp pfs_amd/csrc/gorand.cpp pfs_amd/csrc/knobs.cpp
 HDR := include/pfscdc.h pfs_amd/csrc/pfscdc_internal.h
 
 all: pfs_amd/libpfscdc.so oracle/_build/liboracle.so

@@ -440,7 +440,9 @@ int pfscdc_uw_delete(pfscdc_uwriter* w, const char* path, const char* tag);
 int pfscdc_uw_close(pfscdc_uwriter* w); /* serializes the rest (Close, :171-179) */
 /* Serialized filesets are written in groups of up to PFSCDC_UW_INFLIGHT bytes (knob, default
  * 32 GiB) on a background thread while Puts continue; the event callback may run on that
- * thread, never on two threads at once.  Order: within one (fileset, index, level) stream,
+ * thread, never on two threads at once.  Order: groups in order (with several group writers,
+ * PFSCDC_UW_WORKERS > 1 or a device group, each group's events are held until the groups
+ * before it have emitted theirs); within a group, within one (fileset, index, level) stream
  * and within each fileset's data stream, events come in stream order; a group's data-stream
  * events come fileset by fileset, but its index streams are closed level by level across the
  * group's filesets, so index events of different filesets (and additive and deletive ones)
@@ -476,6 +478,82 @@ int pfscdc_uw_timings(const pfscdc_uwriter* w, double out[9]);
  * destroyed.  pfscdc_uw_cached_arena_bytes: host bytes of the pooled arenas now. */
 int pfscdc_uw_trim_cache(int device, uint64_t* arena_bytes_freed, uint32_t* ctxs_destroyed);
 uint64_t pfscdc_uw_cached_arena_bytes(void);
+
+/* ---- device groups: one process, several GPUs ------------------------------
+ * pachd is one process owning one chunk storage (src/server/pfs/server/driver.go:110-122),
+ * so the GPUs of a node are reached through one caller.  A group holds one ctx per member
+ * device (a device may appear more than once: several ctxs on one GPU) and deals one call's
+ * work across them; results never depend on the dealing or on the number of members.
+ *   Files of a batch: each file is its own chunk stream (writer.go:125-128 resets hash and
+ *     seglen at Annotate), dealt as contiguous file ranges balanced by bytes (pfscdc_deal).
+ *   Unordered writer: serialized filesets (independent chunk streams, fileset/
+ *     unordered_writer.go:83-122, fileset/writer.go:36-50) dealt in groups, round robin.
+ * The chunk-ref index is gathered over xGMI: each member's segment records and Refs stay on
+ * its device and are copied peer to peer (hipMemcpyPeerAsync, direct peer access enabled at
+ * create) into one index on the first member's device (the index device), where their file ids
+ * are rebased, then copied to the host once.  A group is owned by one thread at a time; its
+ * member ctxs belong to it (do not destroy them; do not scan on the group while an unordered
+ * writer made from it is open). */
+
+typedef struct pfscdc_group pfscdc_group;
+
+/* Byte-balanced contiguous split of nitems items (item i = [offsets[i], offsets[i+1]),
+ * nondecreasing) into nparts parts: part r = items [part_begin[r], part_begin[r+1]), starting
+ * at the first item whose prefix reaches ceil(r * total / nparts) bytes (greedy prefix split,
+ * items whole and in order; parts may be empty).  part_begin: nparts + 1 entries.  Host only. */
+int pfscdc_deal(const uint64_t* offsets, uint32_t nitems, uint32_t nparts, uint32_t* part_begin);
+
+/* One ctx per devices[k] (k < n) with params and options (0 or PFSCDC_OPT_REF_IDS).  The
+ * index device is devices[0]. */
+int pfscdc_group_create(const pfscdc_params* params, const int* devices, uint32_t n,
+                        uint32_t options, pfscdc_group** out);
+int pfscdc_group_destroy(pfscdc_group* g);
+uint32_t pfscdc_group_size(const pfscdc_group* g);
+/* Member i's ctx (owned by the group), e.g. for pfscdc_fill_synthetic on its device. */
+pfscdc_ctx* pfscdc_group_ctx(pfscdc_group* g, uint32_t i);
+const char* pfscdc_group_last_error(const pfscdc_group* g);
+
+/* pfscdc_scan of a batch of files in host memory over the group: member k scans the files
+ * [part_begin[k], part_begin[k+1]) of pfscdc_deal(file_offsets, nfiles, n), copying its own
+ * byte range to its device, all members at once.  Blocks until the gathered index is on the
+ * host.  Results as pfscdc_scan's, file ids global. */
+int pfscdc_group_scan(pfscdc_group* g, const void* bytes, uint64_t nbytes,
+                      const uint64_t* file_offsets, uint32_t nfiles);
+/* The same over device-resident bytes: member_bytes[k] (device pointer on member k's device,
+ * 16-B aligned) holds files [part_begin[k], part_begin[k+1]) contiguously, i.e. bytes
+ * [file_offsets[part_begin[k]], file_offsets[part_begin[k+1]]) of the batch.  part_begin:
+ * n + 1 entries (NULL = pfscdc_deal's split). */
+int pfscdc_group_scan_resident(pfscdc_group* g, const void* const* member_bytes,
+                               const uint64_t* file_offsets, uint32_t nfiles,
+                               const uint32_t* part_begin);
+/* Results of the last group scan (valid until the next one): the gathered index ordered by
+ * (file, offset) with global file ids, per-file ranges (nfiles + 1), Refs (NULL unless the
+ * group has PFSCDC_OPT_REF_IDS), and the dealing used (n + 1). */
+uint64_t pfscdc_group_num_segments(const pfscdc_group* g);
+const pfscdc_segment* pfscdc_group_segments(const pfscdc_group* g);
+const uint64_t* pfscdc_group_file_segment_begin(const pfscdc_group* g);
+const pfscdc_ref* pfscdc_group_refs(const pfscdc_group* g);
+const uint32_t* pfscdc_group_part_begin(const pfscdc_group* g);
+/* The gathered index as it lies on the index device (device pointers; nullable outputs). */
+int pfscdc_group_index_device(const pfscdc_group* g, const pfscdc_segment** segs,
+                              const pfscdc_ref** refs, int* device);
+/* Device time of the last group scan: member_ms[k] (n entries) member k's scan-to-hash
+ * (pfscdc_last_timings out[4]); gather_ms the peer copies and rebase on the index device;
+ * gather_bytes the bytes they moved. */
+int pfscdc_group_last_timings(const pfscdc_group* g, float* member_ms, float* gather_ms,
+                              uint64_t* gather_bytes);
+
+/* fileset.Storage.NewUnorderedWriter over a device group (the group needs PFSCDC_OPT_REF_IDS):
+ * as pfscdc_uw_create, with one group writer per member, each writing on its member's ctx and
+ * device (index levels too).  Serialized filesets go out in groups of max(mem_threshold,
+ * PFSCDC_UW_INFLIGHT / n) bytes, round robin over the members, and each Put's bytes are
+ * uploaded to the device of the member that will write them.  Events reach cb in group order,
+ * each group's events as one writer would emit them, so the event stream equals that of
+ * pfscdc_uw_create on one ctx with PFSCDC_UW_INFLIGHT set to the same group bytes; roots
+ * are identical whatever the grouping. */
+int pfscdc_uw_create_group(pfscdc_group* g, int64_t mem_threshold,
+                           const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
+                           pfscdc_uwriter** out);
 
 /* fileset.Clean(p, isDir) (fileset/util.go:67-77) into out (cap bytes incl. NUL). */
 int pfscdc_path_clean(const char* path, int is_directory, char* out, uint64_t cap);

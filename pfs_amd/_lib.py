@@ -54,6 +54,11 @@ EXPORTED = [
     "pfscdc_candidates", "pfscdc_hash_ranges", "pfscdc_fill_synthetic_pieces",
     "pfscdc_last_kernel_spans", "pfscdc_last_kernel_clocks", "pfscdc_order_hash_after",
     "pfscdc_set_knob", "pfscdc_get_knob", "pfscdc_knob_info", "pfscdc_last_scan_mode",
+    "pfscdc_deal", "pfscdc_group_create", "pfscdc_group_destroy", "pfscdc_group_size",
+    "pfscdc_group_ctx", "pfscdc_group_last_error", "pfscdc_group_scan",
+    "pfscdc_group_scan_resident", "pfscdc_group_num_segments", "pfscdc_group_segments",
+    "pfscdc_group_file_segment_begin", "pfscdc_group_refs", "pfscdc_group_part_begin",
+    "pfscdc_group_index_device", "pfscdc_group_last_timings", "pfscdc_uw_create_group",
 ]
 
 
@@ -239,6 +244,22 @@ def load() -> C.CDLL:
             "pfscdc_hash_ranges": (i32, [vp, vp, u64, i32, P(u64), P(u64), u32, vp]),
             "pfscdc_fill_synthetic_pieces": (i32, [vp, vp, P(u64), u32, P(C.c_uint32), P(u64),
                                                    u64, u32]),
+            "pfscdc_deal": (i32, [P(u64), u32, u32, P(C.c_uint32)]),
+            "pfscdc_group_create": (i32, [P(Params), P(C.c_int), u32, u32, P(vp)]),
+            "pfscdc_group_destroy": (i32, [vp]),
+            "pfscdc_group_size": (u32, [vp]),
+            "pfscdc_group_ctx": (vp, [vp, u32]),
+            "pfscdc_group_last_error": (C.c_char_p, [vp]),
+            "pfscdc_group_scan": (i32, [vp, vp, u64, P(u64), u32]),
+            "pfscdc_group_scan_resident": (i32, [vp, P(vp), P(u64), u32, P(C.c_uint32)]),
+            "pfscdc_group_num_segments": (u64, [vp]),
+            "pfscdc_group_segments": (vp, [vp]),
+            "pfscdc_group_file_segment_begin": (P(u64), [vp]),
+            "pfscdc_group_refs": (vp, [vp]),
+            "pfscdc_group_part_begin": (P(C.c_uint32), [vp]),
+            "pfscdc_group_index_device": (i32, [vp, P(vp), P(vp), P(C.c_int)]),
+            "pfscdc_group_last_timings": (i32, [vp, P(C.c_float), P(C.c_float), P(u64)]),
+            "pfscdc_uw_create_group": (i32, [vp, i64, P(Params), UW_CB, vp, P(vp)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "pfscdc_internal.h"
@@ -2254,6 +2255,20 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, const uint32_t* ids,
                         const uint64_t* starts, uint64_t seed, uint32_t mode, hipStream_t st) {
   synth_kernel<<<2048, 256, 0, st>>>(out, offs, nfiles, ids, starts, seed, mode);
+  return hipGetLastError();
+}
+
+// A device group's gathered chunk-ref index: member-local file ids + the member's first file.
+__global__ void rebase_files_kernel(pfscdc_segment* __restrict__ segs, uint64_t n, uint32_t base) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    segs[i].file += base;
+}
+
+hipError_t launch_rebase_files(pfscdc_segment* segs, uint64_t n, uint32_t base, hipStream_t st) {
+  if (n == 0 || base == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 1024);
+  rebase_files_kernel<<<(unsigned)blocks, 256, 0, st>>>(segs, n, base);
   return hipGetLastError();
 }
 

@@ -266,11 +266,20 @@ struct Streams {  // the ctxs of every chunk stream kind; events out
   pfscdc_uw_cb cb = nullptr;
   void* user = nullptr;
   std::mutex* emit_mu = nullptr;  // events of concurrent group writers reach cb one at a time
+  // several group writers: a group's events are held here (the index frames copied) and
+  // released in group order once the groups before it have emitted theirs
+  std::vector<std::pair<pfscdc_uw_event, std::string>>* hold = nullptr;
   int err = 0;
 
   int emit(pfscdc_uw_event& ev, uint32_t fileset) {
     ev.fileset = fileset;
     if (!cb) return PFSCDC_OK;
+    if (hold) {
+      hold->emplace_back(ev, ev.kind == PFSCDC_EV_INDEX
+                                 ? std::string((const char*)ev.bytes, (size_t)ev.len)
+                                 : std::string());
+      return PFSCDC_OK;
+    }
     std::unique_lock<std::mutex> lk;
     if (emit_mu) lk = std::unique_lock<std::mutex>(*emit_mu);
     return cb(user, &ev) != 0 ? PFSCDC_ECALLBACK : PFSCDC_OK;
@@ -759,6 +768,8 @@ struct GroupWorker {
   std::thread th;
   std::atomic<int> rc{PFSCDC_OK};
   std::vector<Buffer> group;
+  std::vector<std::pair<pfscdc_uw_event, std::string>> held;  // this group's events (ordered)
+  int device = 0;
   double stage_ms[8] = {};  // close_group's 6 stages, [6] the index writers, [7] group wall
 };
 
@@ -781,18 +792,24 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   std::vector<std::unique_ptr<GroupWorker>> workers;
   size_t next_worker = 0;
   ~pfscdc_uwriter() {  // the written filesets' arenas serve the next writer
-    if (up_stream) {
-      (void)hipStreamSynchronize(up_stream);
-      (void)hipStreamDestroy(up_stream);
+    for (auto& kv : up_streams) {
+      (void)hipSetDevice(kv.first);
+      (void)hipStreamSynchronize(kv.second);
+      (void)hipStreamDestroy(kv.second);
     }
     for (auto& a : pool)
       if (a->pinned) arena_pool().give(std::move(a));
   }
   double put_copy_ms = 0;  // host copies of the Puts into the arenas
-  int device = 0;
   bool mirror = true;  // the PFSCDC_UW_MIRROR knob (0: upload at group write time instead)
   bool index_grouped = true;  // the PFSCDC_UW_INDEX_GROUPED knob (0: one fileset at a time)
-  hipStream_t up_stream = nullptr;  // the Puts' uploads into the arena mirrors
+  std::map<int, hipStream_t> up_streams;  // the Puts' uploads into the arena mirrors, per device
+  // several group writers: events go out group by group (emit_seq = the next group to emit)
+  bool ordered = false;
+  std::mutex seq_mu;
+  std::condition_variable seq_cv;
+  uint64_t emit_seq = 0, next_seq = 0;
+  bool emit_failed = false;
   uint64_t pending_bytes = 0, inflight_bytes = 32ull << 30;
   std::vector<std::pair<std::vector<std::pair<std::string, std::string>>,
                         std::vector<std::pair<std::string, std::string>>>> keys;  // files, deletes
@@ -819,11 +836,20 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
   }
 
   std::unique_ptr<Arena> new_arena() {
+    // the mirror lives on the device of the group writer the next flush goes to (all of a
+    // group's filesets are written by one writer)
+    const int device = workers[next_worker]->device;
     {
       std::lock_guard<std::mutex> lk(pool_mu);
-      if (!pool.empty()) {
-        std::unique_ptr<Arena> a = std::move(pool.back());
-        pool.pop_back();
+      if (!pool.empty()) {  // a written fileset's arena, preferably one mirrored on device
+        size_t pick = pool.size() - 1;
+        for (size_t i = pool.size(); i-- > 0;)
+          if (pool[i]->device == device) {
+            pick = i;
+            break;
+          }
+        std::unique_ptr<Arena> a = std::move(pool[pick]);
+        pool.erase(pool.begin() + (ptrdiff_t)pick);
         a->used = 0;
         return a;
       }
@@ -868,10 +894,38 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
 
   // Writes one group of serialized buffers: a fileset.Writer each, their data streams
   // through one grouped close, then their indexes; the arenas go back to the pool.
-  int write_group(GroupWorker& gw, std::vector<Buffer>& group, uint32_t fs0) {
+  // Group seq's held events, once groups < seq have emitted theirs (several group writers).
+  // A group that failed, or follows a failed emission, emits nothing but still takes its turn.
+  int release_events(GroupWorker& gw, uint64_t seq, int rc) {
+    std::unique_lock<std::mutex> lk(seq_mu);
+    seq_cv.wait(lk, [&] { return emit_seq == seq; });
+    if (!rc && !emit_failed) {
+      std::lock_guard<std::mutex> ek(emit_mu);
+      for (auto& e : gw.held) {
+        if (e.first.kind == PFSCDC_EV_INDEX) e.first.bytes = (const uint8_t*)e.second.data();
+        if (gw.st.cb(gw.st.user, &e.first) != 0) {
+          rc = PFSCDC_ECALLBACK;
+          break;
+        }
+      }
+    }
+    if (rc) emit_failed = true;
+    gw.held.clear();
+    emit_seq++;
+    seq_cv.notify_all();
+    return rc;
+  }
+
+  int write_group(GroupWorker& gw, std::vector<Buffer>& group, uint32_t fs0, uint64_t seq) {
+    int rc = write_group_body(gw, group, fs0);
+    return ordered && gw.st.cb ? release_events(gw, seq, rc) : rc;
+  }
+
+  int write_group_body(GroupWorker& gw, std::vector<Buffer>& group, uint32_t fs0) {
     using clk = std::chrono::steady_clock;
     const auto g0 = clk::now();
     Streams& st = gw.st;
+    st.hold = ordered ? &gw.held : nullptr;
     std::vector<std::unique_ptr<FilesetWriter>> fws;
     std::vector<pfscdc_writer*> cws;
     std::vector<hipEvent_t> evs;  // the group's arena uploads
@@ -952,11 +1006,12 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
     if (gw.th.joinable()) gw.th.join();
     if (int rc = gw.rc.load()) return rc;
     const uint32_t fs0 = next_fileset - (uint32_t)pending.size();
+    const uint64_t seq = next_seq++;
     gw.group.clear();
     gw.group.swap(pending);
     pending_bytes = 0;
-    if (!async) return write_group(gw, gw.group, fs0);
-    gw.th = std::thread([this, &gw, fs0] { gw.rc = write_group(gw, gw.group, fs0); });
+    if (!async) return write_group(gw, gw.group, fs0, seq);
+    gw.th = std::thread([this, &gw, fs0, seq] { gw.rc = write_group(gw, gw.group, fs0, seq); });
     return PFSCDC_OK;
   }
 
@@ -977,12 +1032,13 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
         put_copy_ms += std::chrono::duration<double, std::milli>(
                            std::chrono::steady_clock::now() - c0).count();
         if (a.dev) {  // on to the device while the next Puts copy
-          if (!up_stream && (hipSetDevice(device) != hipSuccess ||
-                             hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking) != hipSuccess))
+          hipStream_t& up = up_streams[a.device];
+          if (hipSetDevice(a.device) != hipSuccess ||
+              (!up && hipStreamCreateWithFlags(&up, hipStreamNonBlocking) != hipSuccess))
             return PFSCDC_EHIP;
-          if (hipMemcpyAsync(a.dev + a.used, a.p + a.used, got, hipMemcpyHostToDevice,
-                             up_stream) != hipSuccess ||
-              hipEventRecord(a.ev, up_stream) != hipSuccess)
+          if (hipMemcpyAsync(a.dev + a.used, a.p + a.used, got, hipMemcpyHostToDevice, up) !=
+                  hipSuccess ||
+              hipEventRecord(a.ev, up) != hipSuccess)
             return PFSCDC_EHIP;
         }
         if (!w->empty() && w->back().off + w->back().len == a.used) w->back().len += got;
@@ -1023,12 +1079,11 @@ struct pfscdc_uwriter {  // unordered_writer.go:15-26
 
 extern "C" {
 
-int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
-                     const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
-                     pfscdc_uwriter** out) {
-  if (!data_ctx || !out || mem_threshold < 0) return PFSCDC_EINVAL;
-  if (!(pfscdc::ctx_options(data_ctx) & PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
-  pfscdc_uwriter* w = new pfscdc_uwriter();
+}  // extern "C"
+
+namespace {
+
+pfscdc_params index_params_or_default(const pfscdc_params* index_params) {
   pfscdc_params ip;
   if (index_params) {
     ip = *index_params;
@@ -1037,6 +1092,53 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
     ip.average_bits = 20;
     ip.seed = 0;
   }
+  return ip;
+}
+
+void finish_create(pfscdc_uwriter* w, int64_t mem_threshold) {
+  if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
+  w->inflight_bytes = (uint64_t)pfscdc::knob(pfscdc::Knob::UwInflight);
+  w->mirror = pfscdc::knob(pfscdc::Knob::UwMirror) != 0;
+  w->index_grouped = pfscdc::knob(pfscdc::Knob::UwIndexGrouped) != 0;
+  w->ordered = w->workers.size() > 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfscdc_uw_create_group(pfscdc_group* g, int64_t mem_threshold,
+                           const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
+                           pfscdc_uwriter** out) {
+  const uint32_t n = pfscdc_group_size(g);
+  if (!g || !out || mem_threshold < 0 || n == 0) return PFSCDC_EINVAL;
+  if (!(pfscdc::ctx_options(pfscdc_group_ctx(g, 0)) & PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
+  pfscdc_uwriter* w = new pfscdc_uwriter();
+  const pfscdc_params ip = index_params_or_default(index_params);
+  for (uint32_t k = 0; k < n; k++) {  // one group writer per member, on the member's ctx
+    auto gw = std::make_unique<GroupWorker>();
+    gw->st.cb = cb;
+    gw->st.user = user;
+    gw->st.emit_mu = &w->emit_mu;
+    gw->st.index_params = ip;
+    gw->st.data_ctx = pfscdc_group_ctx(g, k);
+    gw->device = pfscdc::ctx_device(gw->st.data_ctx);
+    w->workers.push_back(std::move(gw));
+  }
+  finish_create(w, mem_threshold);
+  // n groups in flight hold what one writer's group would
+  w->inflight_bytes = std::max<uint64_t>(w->inflight_bytes / n, (uint64_t)w->mem_threshold);
+  *out = w;
+  return PFSCDC_OK;
+}
+
+int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
+                     const pfscdc_params* index_params, pfscdc_uw_cb cb, void* user,
+                     pfscdc_uwriter** out) {
+  if (!data_ctx || !out || mem_threshold < 0) return PFSCDC_EINVAL;
+  if (!(pfscdc::ctx_options(data_ctx) & PFSCDC_OPT_REF_IDS)) return PFSCDC_EINVAL;
+  pfscdc_uwriter* w = new pfscdc_uwriter();
+  const pfscdc_params ip = index_params_or_default(index_params);
   // group writers: the first on the caller's data ctx, the others on ctxs of their own
   // (the PFSCDC_UW_WORKERS knob, default 1: two groups in flight contend for the CUs, and each
   // group's chunk.Create chains then run longer; c4, 8 GiB: 15.2 GiB/s with one, 8.9 with two)
@@ -1059,13 +1161,10 @@ int pfscdc_uw_create(pfscdc_ctx* data_ctx, int64_t mem_threshold,
       gw->st.data_ctx = c;
       gw->st.own_data_ctx = true;
     }
+    gw->device = pfscdc::ctx_device(gw->st.data_ctx);
     w->workers.push_back(std::move(gw));
   }
-  w->device = pfscdc::ctx_device(data_ctx);
-  if (mem_threshold) w->mem_threshold = w->mem_available = mem_threshold;
-  w->inflight_bytes = (uint64_t)pfscdc::knob(pfscdc::Knob::UwInflight);
-  w->mirror = pfscdc::knob(pfscdc::Knob::UwMirror) != 0;
-  w->index_grouped = pfscdc::knob(pfscdc::Knob::UwIndexGrouped) != 0;
+  finish_create(w, mem_threshold);
   *out = w;
   return PFSCDC_OK;
 }

@@ -1,0 +1,383 @@
+// group.cpp — one process, several GPUs: a device group of contexts (C ABI pfscdc_group_*).
+//
+// pachd is one process that owns one chunk storage (reference
+// src/server/pfs/server/driver.go:110-122), so a commit reaches the GPUs of a node through one
+// caller, not one process per GPU.  A group holds one pfscdc_ctx per member device and deals
+// the work of one call across them:
+//   * a batch of independent files (configs[1], and any Put batch): contiguous file ranges
+//     balanced by bytes (pfscdc_deal), each scanned on its member's stream; the per-file
+//     results depend on the file's bytes alone (writer.go:125-128 resets hash and seglen at
+//     every Annotate), so the dealing never changes a result;
+//   * an unordered writer (fileset.cpp, pfscdc_uw_create_group): serialized filesets, each an
+//     independent chunk stream (unordered_writer.go:83-122), in groups round robin.
+// The gather of the chunk-ref index: every member's segment records (and Refs) stay on its
+// device and are copied peer to peer (hipMemcpyPeerAsync: xGMI between MI355X devices, a
+// device-local copy when members share a GPU) into one index on the first member's device,
+// their member-local file ids rebased there, then brought to the host in one copy.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pfscdc_internal.h"
+
+using namespace pfscdc;
+
+struct pfscdc_group {
+  std::vector<pfscdc_ctx*> members;
+  std::vector<int> devices;
+  int index_device = 0;
+  hipStream_t stream = nullptr;  // the gather (index device)
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  std::string err;
+  // the last scan
+  std::vector<uint32_t> part_begin;
+  std::vector<uint64_t> seg_begin;
+  std::vector<float> member_ms;
+  float gather_ms = 0.f;
+  uint64_t nsegs = 0;
+  bool have_refs = false;
+  pfscdc_segment* d_index = nullptr;  // on index_device
+  pfscdc_ref* d_refs = nullptr;
+  uint64_t d_cap = 0;
+  pfscdc_segment* h_index = nullptr;  // page-locked
+  pfscdc_ref* h_refs = nullptr;
+  uint64_t h_cap = 0;
+  uint64_t bytes_copied = 0;  // bytes the gather moved (records + refs)
+
+  int fail(int code, const std::string& msg) {
+    err = msg;
+    return code;
+  }
+  void release_buffers() {
+    if (d_index || d_refs) (void)hipSetDevice(index_device);
+    if (d_index) (void)hipFree(d_index);
+    if (d_refs) (void)hipFree(d_refs);
+    if (h_index) (void)hipHostFree(h_index);
+    if (h_refs) (void)hipHostFree(h_refs);
+    d_index = nullptr;
+    d_refs = nullptr;
+    h_index = nullptr;
+    h_refs = nullptr;
+    d_cap = h_cap = 0;
+  }
+};
+
+namespace {
+
+#define GROUP_HIP(g, expr)                                                                  \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return (g)->fail(e_ == hipErrorOutOfMemory ? PFSCDC_ENOMEM : PFSCDC_EHIP,             \
+                       std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+int check_offsets(pfscdc_group* g, const uint64_t* offs, uint32_t nfiles, uint64_t nbytes) {
+  if (!offs) return g->fail(PFSCDC_EINVAL, "file_offsets is NULL");
+  if (offs[0] != 0 || offs[nfiles] != nbytes)
+    return g->fail(PFSCDC_EINVAL, "file_offsets must start at 0 and end at nbytes");
+  for (uint32_t f = 0; f < nfiles; f++)
+    if (offs[f + 1] < offs[f]) return g->fail(PFSCDC_EINVAL, "file_offsets must be nondecreasing");
+  return PFSCDC_OK;
+}
+
+// Member k scans files [pb[k], pb[k+1]) from src (its bytes, host or device), keeping the
+// records on its device.
+int member_scan(pfscdc_ctx* c, const uint8_t* src, int on_device, const uint64_t* offs,
+                uint32_t f0, uint32_t f1, float* ms) {
+  std::vector<uint64_t> local(f1 - f0 + 1);
+  for (uint32_t f = f0; f <= f1; f++) local[f - f0] = offs[f] - offs[f0];
+  int rc = pfscdc_scan_async(c, src, local.back(), on_device, local.data(), f1 - f0);
+  if (!rc) rc = wait_impl(c, false);
+  float t[5] = {0, 0, 0, 0, 0};
+  if (!rc && pfscdc_last_timings(c, t) == PFSCDC_OK) *ms = t[4];
+  return rc;
+}
+
+int ensure_index(pfscdc_group* g, uint64_t n, bool refs) {
+  if (n > g->d_cap || (refs && !g->d_refs && n)) {
+    GROUP_HIP(g, hipSetDevice(g->index_device));
+    const uint64_t want = n + n / 4 + 1;
+    if (g->d_index) (void)hipFree(g->d_index);
+    if (g->d_refs) (void)hipFree(g->d_refs);
+    g->d_index = nullptr;
+    g->d_refs = nullptr;
+    g->d_cap = 0;
+    GROUP_HIP(g, hipMalloc((void**)&g->d_index, want * sizeof(pfscdc_segment)));
+    if (refs) GROUP_HIP(g, hipMalloc((void**)&g->d_refs, want * sizeof(pfscdc_ref)));
+    g->d_cap = want;
+  }
+  if (n > g->h_cap || (refs && !g->h_refs && n)) {
+    const uint64_t want = n + n / 4 + 1;
+    if (g->h_index) (void)hipHostFree(g->h_index);
+    if (g->h_refs) (void)hipHostFree(g->h_refs);
+    g->h_index = nullptr;
+    g->h_refs = nullptr;
+    g->h_cap = 0;
+    GROUP_HIP(g, hipHostMalloc((void**)&g->h_index, want * sizeof(pfscdc_segment),
+                               hipHostMallocDefault));
+    if (refs)
+      GROUP_HIP(g, hipHostMalloc((void**)&g->h_refs, want * sizeof(pfscdc_ref), hipHostMallocDefault));
+    g->h_cap = want;
+  }
+  return PFSCDC_OK;
+}
+
+// The scan of every member (one host thread each: a member's H2D copy from pageable memory
+// blocks its thread only), then the gather.
+int group_scan(pfscdc_group* g, const uint8_t* host, const void* const* member_bytes,
+               const uint64_t* offs, uint32_t nfiles) {
+  const uint32_t n = (uint32_t)g->members.size();
+  const uint32_t* pb = g->part_begin.data();
+  g->member_ms.assign(n, 0.f);
+  std::vector<int> rcs(n, PFSCDC_OK);
+  std::vector<std::thread> th;
+  for (uint32_t k = 0; k < n; k++) {
+    if (pb[k + 1] == pb[k]) continue;
+    const uint8_t* src = host ? host + offs[pb[k]] : (const uint8_t*)member_bytes[k];
+    const int on_dev = host ? 0 : 1;
+    auto job = [g, k, src, on_dev, offs, pb, &rcs] {
+      rcs[k] = member_scan(g->members[k], src, on_dev, offs, pb[k], pb[k + 1], &g->member_ms[k]);
+    };
+    if (k + 1 == n) job();  // the caller's thread takes the last member
+    else th.emplace_back(job);
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t k = 0; k < n; k++)
+    if (rcs[k])
+      return g->fail(rcs[k], "member " + std::to_string(k) + " (device " +
+                                 std::to_string(g->devices[k]) + "): " +
+                                 pfscdc_last_error(g->members[k]));
+  // the global per-file segment ranges, then the records of every member peer to peer
+  g->seg_begin.assign((size_t)nfiles + 1, 0);
+  std::vector<uint64_t> base(n + 1, 0);
+  g->have_refs = (pfscdc::ctx_options(g->members[0]) & PFSCDC_OPT_REF_IDS) != 0;
+  for (uint32_t k = 0; k < n; k++) {
+    uint64_t cnt = 0;
+    if (pb[k + 1] > pb[k]) {
+      const uint64_t* lb = pfscdc_file_segment_begin(g->members[k]);
+      for (uint32_t f = pb[k]; f < pb[k + 1]; f++) g->seg_begin[f] = base[k] + lb[f - pb[k]];
+      cnt = lb[pb[k + 1] - pb[k]];
+    }
+    base[k + 1] = base[k] + cnt;
+  }
+  const uint64_t total = base[n];
+  g->seg_begin[nfiles] = total;
+  g->nsegs = total;
+  int rc = ensure_index(g, total, g->have_refs);
+  if (rc) return rc;
+  GROUP_HIP(g, hipSetDevice(g->index_device));
+  GROUP_HIP(g, hipEventRecord(g->ev[0], g->stream));
+  g->bytes_copied = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    const uint64_t cnt = base[k + 1] - base[k];
+    if (!cnt) continue;
+    pfscdc_segment* ds = nullptr;
+    pfscdc_ref* dr = nullptr;
+    uint64_t got = 0;
+    ctx_device_results(g->members[k], &ds, &dr, &got);
+    if (got != cnt) return g->fail(PFSCDC_EHIP, "member segment count changed");
+    GROUP_HIP(g, hipMemcpyPeerAsync(g->d_index + base[k], g->index_device, ds, g->devices[k],
+                                    cnt * sizeof(pfscdc_segment), g->stream));
+    g->bytes_copied += cnt * sizeof(pfscdc_segment);
+    if (g->have_refs && dr) {
+      GROUP_HIP(g, hipMemcpyPeerAsync(g->d_refs + base[k], g->index_device, dr, g->devices[k],
+                                      cnt * sizeof(pfscdc_ref), g->stream));
+      g->bytes_copied += cnt * sizeof(pfscdc_ref);
+    }
+    GROUP_HIP(g, launch_rebase_files(g->d_index + base[k], cnt, pb[k], g->stream));
+  }
+  GROUP_HIP(g, hipEventRecord(g->ev[1], g->stream));
+  if (total) {
+    GROUP_HIP(g, hipMemcpyAsync(g->h_index, g->d_index, total * sizeof(pfscdc_segment),
+                                hipMemcpyDeviceToHost, g->stream));
+    if (g->have_refs)
+      GROUP_HIP(g, hipMemcpyAsync(g->h_refs, g->d_refs, total * sizeof(pfscdc_ref),
+                                  hipMemcpyDeviceToHost, g->stream));
+  }
+  GROUP_HIP(g, hipStreamSynchronize(g->stream));
+  GROUP_HIP(g, hipEventElapsedTime(&g->gather_ms, g->ev[0], g->ev[1]));
+  return PFSCDC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfscdc_deal(const uint64_t* offsets, uint32_t nitems, uint32_t nparts, uint32_t* part_begin) {
+  if (!offsets || !part_begin || nparts == 0) return PFSCDC_EINVAL;
+  for (uint32_t i = 0; i < nitems; i++)
+    if (offsets[i + 1] < offsets[i]) return PFSCDC_EINVAL;
+  // part r starts at the first item whose prefix reaches r/nparts of the bytes (greedy prefix
+  // split; items stay whole and in order)
+  const uint64_t o0 = offsets[0], total = offsets[nitems] - o0;
+  part_begin[0] = 0;
+  for (uint32_t r = 1; r < nparts; r++) {
+    const unsigned __int128 t = (unsigned __int128)total * r;
+    const uint64_t target = (uint64_t)((t + nparts - 1) / nparts);  // ceil
+    uint32_t lo = 0, hi = nitems;  // first i in [0, nitems] with prefix(i) >= target
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (offsets[mid] - o0 >= target) hi = mid;
+      else lo = mid + 1;
+    }
+    part_begin[r] = lo < part_begin[r - 1] ? part_begin[r - 1] : lo;
+  }
+  part_begin[nparts] = nitems;
+  return PFSCDC_OK;
+}
+
+int pfscdc_group_create(const pfscdc_params* params, const int* devices, uint32_t n,
+                        uint32_t options, pfscdc_group** out) {
+  if (!out || !devices || n == 0 || !params) return PFSCDC_EINVAL;
+  *out = nullptr;
+  if (options & ~PFSCDC_OPT_REF_IDS) return PFSCDC_EINVAL;  // no cuts-only / in-place groups
+  pfscdc_group* g = new pfscdc_group();
+  for (uint32_t k = 0; k < n; k++) {
+    pfscdc_ctx* c = nullptr;
+    int rc = pfscdc_ctx_create(params, devices[k], &c);
+    if (!rc) rc = pfscdc_set_options(c, options);
+    if (rc) {
+      if (c) pfscdc_ctx_destroy(c);
+      pfscdc_group_destroy(g);
+      return rc;
+    }
+    g->members.push_back(c);
+    g->devices.push_back(devices[k]);
+  }
+  g->index_device = devices[0];
+  // direct peer access from the index device to every other member device (xGMI); without it
+  // hipMemcpyPeerAsync still works, staged through host memory
+  for (uint32_t k = 1; k < n; k++) {
+    if (devices[k] == g->index_device) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, g->index_device, devices[k]) == hipSuccess && can) {
+      (void)hipSetDevice(g->index_device);
+      const hipError_t e = hipDeviceEnablePeerAccess(devices[k], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        pfscdc_group_destroy(g);
+        return PFSCDC_EHIP;
+      }
+      (void)hipGetLastError();  // "already enabled" is not an error here
+    }
+  }
+  if (hipSetDevice(g->index_device) != hipSuccess ||
+      hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&g->ev[0]) != hipSuccess || hipEventCreate(&g->ev[1]) != hipSuccess) {
+    pfscdc_group_destroy(g);
+    return PFSCDC_EHIP;
+  }
+  *out = g;
+  return PFSCDC_OK;
+}
+
+int pfscdc_group_destroy(pfscdc_group* g) {
+  if (!g) return PFSCDC_EINVAL;
+  if (g->stream) {
+    (void)hipSetDevice(g->index_device);
+    (void)hipStreamSynchronize(g->stream);
+  }
+  g->release_buffers();
+  for (auto& e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  for (pfscdc_ctx* c : g->members) pfscdc_ctx_destroy(c);
+  delete g;
+  return PFSCDC_OK;
+}
+
+uint32_t pfscdc_group_size(const pfscdc_group* g) { return g ? (uint32_t)g->members.size() : 0; }
+
+pfscdc_ctx* pfscdc_group_ctx(pfscdc_group* g, uint32_t i) {
+  return g && i < g->members.size() ? g->members[i] : nullptr;
+}
+
+const char* pfscdc_group_last_error(const pfscdc_group* g) { return g ? g->err.c_str() : "null group"; }
+
+int pfscdc_group_scan(pfscdc_group* g, const void* bytes, uint64_t nbytes,
+                      const uint64_t* file_offsets, uint32_t nfiles) {
+  if (!g) return PFSCDC_EINVAL;
+  g->err.clear();
+  g->nsegs = 0;
+  if (nbytes && !bytes) return g->fail(PFSCDC_EINVAL, "bytes is NULL");
+  int rc = check_offsets(g, file_offsets, nfiles, nbytes);
+  if (rc) return rc;
+  const uint32_t n = (uint32_t)g->members.size();
+  g->part_begin.assign(n + 1, 0);
+  rc = pfscdc_deal(file_offsets, nfiles, n, g->part_begin.data());
+  if (rc) return g->fail(rc, "deal");
+  return group_scan(g, (const uint8_t*)bytes, nullptr, file_offsets, nfiles);
+}
+
+int pfscdc_group_scan_resident(pfscdc_group* g, const void* const* member_bytes,
+                               const uint64_t* file_offsets, uint32_t nfiles,
+                               const uint32_t* part_begin) {
+  if (!g || !member_bytes) return PFSCDC_EINVAL;
+  g->err.clear();
+  g->nsegs = 0;
+  if (!file_offsets) return g->fail(PFSCDC_EINVAL, "file_offsets is NULL");
+  int rc = check_offsets(g, file_offsets, nfiles, file_offsets[nfiles]);
+  if (rc) return rc;
+  const uint32_t n = (uint32_t)g->members.size();
+  g->part_begin.assign(n + 1, 0);
+  if (part_begin) {
+    if (part_begin[0] != 0 || part_begin[n] != nfiles)
+      return g->fail(PFSCDC_EINVAL, "part_begin must run from 0 to nfiles");
+    for (uint32_t k = 0; k < n; k++)
+      if (part_begin[k + 1] < part_begin[k])
+        return g->fail(PFSCDC_EINVAL, "part_begin must be nondecreasing");
+    std::memcpy(g->part_begin.data(), part_begin, sizeof(uint32_t) * (n + 1));
+  } else {
+    rc = pfscdc_deal(file_offsets, nfiles, n, g->part_begin.data());
+    if (rc) return g->fail(rc, "deal");
+  }
+  for (uint32_t k = 0; k < n; k++)
+    if (g->part_begin[k + 1] > g->part_begin[k] &&
+        file_offsets[g->part_begin[k + 1]] > file_offsets[g->part_begin[k]] && !member_bytes[k])
+      return g->fail(PFSCDC_EINVAL, "member " + std::to_string(k) + " has bytes but no buffer");
+  return group_scan(g, nullptr, member_bytes, file_offsets, nfiles);
+}
+
+uint64_t pfscdc_group_num_segments(const pfscdc_group* g) { return g ? g->nsegs : 0; }
+
+const pfscdc_segment* pfscdc_group_segments(const pfscdc_group* g) {
+  return g && g->nsegs ? g->h_index : nullptr;
+}
+
+const uint64_t* pfscdc_group_file_segment_begin(const pfscdc_group* g) {
+  return g && !g->seg_begin.empty() ? g->seg_begin.data() : nullptr;
+}
+
+const pfscdc_ref* pfscdc_group_refs(const pfscdc_group* g) {
+  return g && g->have_refs && g->nsegs ? g->h_refs : nullptr;
+}
+
+const uint32_t* pfscdc_group_part_begin(const pfscdc_group* g) {
+  return g && !g->part_begin.empty() ? g->part_begin.data() : nullptr;
+}
+
+int pfscdc_group_index_device(const pfscdc_group* g, const pfscdc_segment** segs,
+                              const pfscdc_ref** refs, int* device) {
+  if (!g) return PFSCDC_EINVAL;
+  if (segs) *segs = g->nsegs ? g->d_index : nullptr;
+  if (refs) *refs = g->nsegs && g->have_refs ? g->d_refs : nullptr;
+  if (device) *device = g->index_device;
+  return PFSCDC_OK;
+}
+
+int pfscdc_group_last_timings(const pfscdc_group* g, float* member_ms, float* gather_ms,
+                              uint64_t* gather_bytes) {
+  if (!g) return PFSCDC_EINVAL;
+  if (member_ms)
+    for (size_t k = 0; k < g->members.size(); k++)
+      member_ms[k] = k < g->member_ms.size() ? g->member_ms[k] : 0.f;
+  if (gather_ms) *gather_ms = g->gather_ms;
+  if (gather_bytes) *gather_bytes = g->bytes_copied;
+  return PFSCDC_OK;
+}
+
+}  // extern "C"

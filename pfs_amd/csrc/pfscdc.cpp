@@ -139,6 +139,7 @@ struct pfscdc_ctx {
   hipEvent_t pev[3] = {nullptr, nullptr, nullptr};  // commit_refs: start, long / short unions
   bool have_refs = false;
   bool scan_valid = false;  // h_offs/h_segs/h_seg_begin hold the last scan's results
+  bool host_records = true;  // h_segs / h_refs were fetched (not by a device group's member)
   PinnedBuf<uint64_t> h_offs, h_seg_base, h_seg_begin;
   PinnedBuf<pfscdc_segment> h_segs;
   hipEvent_t ev[8] = {};
@@ -600,7 +601,13 @@ int pfscdc_scan_async(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int byt
   return rc;
 }
 
-int pfscdc_wait(pfscdc_ctx* c) {
+int pfscdc_wait(pfscdc_ctx* c) { return pfscdc::wait_impl(c, true); }
+
+}  // extern "C"
+
+// fetch = false (a device group's member): the segment records and refs stay on the device
+// for the group's gather; only the per-file segment counts come back.
+int pfscdc::wait_impl(pfscdc_ctx* c, bool fetch) {
   if (!c) return PFSCDC_EINVAL;
   if (!c->pending) return PFSCDC_OK;
   c->pending = false;
@@ -609,10 +616,10 @@ int pfscdc_wait(pfscdc_ctx* c) {
   const uint64_t total = c->nfiles ? c->h_seg_begin.p[c->nfiles] : 0;
   if (total > c->slot_cap) return fail(c, PFSCDC_EHIP, "segment count exceeds slot capacity");
   HIP_OK(c, c->h_segs.ensure(total));
-  if (total)
+  if (total && fetch)
     HIP_OK(c, hipMemcpyAsync(c->h_segs.p, c->d_segs.p, total * sizeof(pfscdc_segment),
                              hipMemcpyDeviceToHost, c->stream));
-  if (c->have_refs) {
+  if (c->have_refs && fetch) {
     HIP_OK(c, c->h_refs.ensure(total));
     if (total)
       HIP_OK(c, hipMemcpyAsync(c->h_refs.p, c->d_refs.p, total * sizeof(pfscdc_ref),
@@ -629,9 +636,12 @@ int pfscdc_wait(pfscdc_ctx* c) {
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->scanned_bytes = skipped ? c->h_span.p[kSpanSlots] - c->h_span.p[kSpanSlots + 3] : c->nbytes;
   c->nsegs = total;
-  c->scan_valid = true;
+  c->scan_valid = fetch;
+  c->host_records = fetch;
   return PFSCDC_OK;
 }
+
+extern "C" {
 
 int pfscdc_last_kernel_spans(pfscdc_ctx* c, float out[2]) {
   if (!c || !out) return PFSCDC_EINVAL;
@@ -678,7 +688,7 @@ int pfscdc_set_options(pfscdc_ctx* c, uint32_t options) {
 }
 
 const pfscdc_ref* pfscdc_refs(const pfscdc_ctx* c) {
-  return c && c->have_refs && !c->pending ? c->h_refs.p : nullptr;
+  return c && c->have_refs && !c->pending && c->host_records ? c->h_refs.p : nullptr;
 }
 
 int pfscdc_last_ref_ms(pfscdc_ctx* c, float* ms) {
@@ -687,7 +697,9 @@ int pfscdc_last_ref_ms(pfscdc_ctx* c, float* ms) {
   if (c->have_refs) HIP_OK(c, hipEventElapsedTime(ms, c->ev[4], c->ev[6]));
   return PFSCDC_OK;
 }
-const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* c) { return c ? c->h_segs.p : nullptr; }
+const pfscdc_segment* pfscdc_segments(const pfscdc_ctx* c) {
+  return c && c->host_records ? c->h_segs.p : nullptr;
+}
 const uint64_t* pfscdc_file_segment_begin(const pfscdc_ctx* c) {
   return c ? c->h_seg_begin.p : nullptr;
 }
@@ -1438,6 +1450,13 @@ uint32_t ctx_options(const pfscdc_ctx* c) { return c->options; }
 bool ctx_scan_valid(const pfscdc_ctx* c) { return c->scan_valid && !c->pending; }
 uint32_t ctx_nfiles(const pfscdc_ctx* c) { return c->nfiles; }
 uint64_t ctx_file_offset(const pfscdc_ctx* c, uint32_t f) { return c->h_offs.p[f]; }
+void ctx_device_results(const pfscdc_ctx* c, pfscdc_segment** segs, pfscdc_ref** refs,
+                        uint64_t* n) {
+  *segs = c->d_segs.p;
+  *refs = c->have_refs ? c->d_refs.p : nullptr;
+  *n = c->nsegs;
+}
+hipStream_t ctx_stream(const pfscdc_ctx* c) { return c->stream; }
 
 int scan_sync(pfscdc_ctx* c, const void* bytes, uint64_t nbytes, int bytes_on_device,
               const uint64_t* file_offsets, uint32_t nfiles, uint32_t options) {

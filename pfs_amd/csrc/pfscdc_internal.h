@@ -96,6 +96,13 @@ uint32_t ctx_options(const pfscdc_ctx* ctx);
 bool ctx_scan_valid(const pfscdc_ctx* ctx);
 uint32_t ctx_nfiles(const pfscdc_ctx* ctx);
 uint64_t ctx_file_offset(const pfscdc_ctx* ctx, uint32_t f);
+// pfscdc_wait; fetch = false leaves the segment records and refs on the device (the host
+// gets the per-file segment counts only): a device group gathers them over xGMI
+int wait_impl(pfscdc_ctx* ctx, bool fetch);
+// the last waited-for scan's device records: segments, refs (nullptr without Ref ids), count
+void ctx_device_results(const pfscdc_ctx* ctx, pfscdc_segment** segs, pfscdc_ref** refs,
+                        uint64_t* n);
+hipStream_t ctx_stream(const pfscdc_ctx* ctx);
 
 hipError_t prepare_kernels();  // per-device kernel attributes; call after hipSetDevice
 
@@ -192,6 +199,9 @@ hipError_t launch_get(const uint8_t* ctext, const uint64_t* offs, pfscdc_segment
                       const uint64_t* seg_count, uint64_t nsegs, uint32_t* order, uint32_t* counter,
                       int num_cus, uint64_t nbytes, pfscdc_ref* refs, uint8_t* ptext, hipStream_t st,
                       int waves = 0);
+// segs[i].file += base for i < n (a device group's gathered index: member-local file ids
+// become the commit's)
+hipError_t launch_rebase_files(pfscdc_segment* segs, uint64_t n, uint32_t base, hipStream_t st);
 hipError_t launch_synth(uint8_t* out, const uint64_t* offs, uint32_t nfiles, const uint32_t* ids,
                         const uint64_t* starts, uint64_t seed, uint32_t mode, hipStream_t st);
 

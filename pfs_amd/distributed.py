@@ -45,7 +45,7 @@ def shard_files(file_sizes: Sequence[int], world_size: int) -> list[tuple[int, i
     total = int(cum[-1])
     bounds = [0]
     for r in range(1, world_size):
-        target = total * r / world_size
+        target = -(-total * r // world_size)  # ceil, exact (the C ABI's pfscdc_deal)
         # first file index whose prefix reaches the target, kept monotone
         b = int(np.searchsorted(cum, target, side="left"))
         b = max(bounds[-1], min(b, n))

@@ -21,7 +21,7 @@ from __future__ import annotations
 import ctypes as C
 import weakref
 from dataclasses import dataclass
-from typing import Optional
+from typing import Optional, Sequence
 
 import numpy as np
 
@@ -50,25 +50,34 @@ def clean(p: str, is_dir: bool) -> str:
 
 
 class Storage:
-    """``fileset.Storage`` restricted to the write path, bound to one GPU."""
+    """``fileset.Storage`` restricted to the write path, bound to one GPU, or with
+    ``devices`` to a device group (one process, several GPUs: pfscdc_uw_create_group deals
+    the serialized filesets over them; the filesets and events equal one GPU's)."""
 
     def __init__(self, device: int = 0, params: ChunkParams = ChunkParams(),
                  mem_threshold: int = DEFAULT_MEMORY_THRESHOLD,
-                 index_params: Optional[ChunkParams] = None):
+                 index_params: Optional[ChunkParams] = None,
+                 devices: Optional[Sequence[int]] = None):
         self.device, self.params = device, params
+        self.devices = list(devices) if devices is not None else None
         self.mem_threshold, self.index_params = mem_threshold, index_params
-        self._idle: list = []  # data-stream contexts of closed writers, for the next writer
+        self._idle: list = []  # data-stream contexts (or groups) of closed writers, for the next
 
     def new_unordered_writer(self) -> "UnorderedWriter":
         return UnorderedWriter(self)
 
-    def _take_chunker(self) -> Chunker:
+    def _take_chunker(self):
         # a context (stream, events, device staging) per GPU, reused writer after writer, as
         # a pachd process would hold it; a writer still open gets a context of its own
-        return self._idle.pop() if self._idle else Chunker(self.params, self.device, ref_ids=True)
+        if self._idle:
+            return self._idle.pop()
+        if self.devices is not None:
+            from .group import DeviceGroup
+            return DeviceGroup(self.devices, self.params, ref_ids=True)
+        return Chunker(self.params, self.device, ref_ids=True)
 
-    def _give_chunker(self, c: Chunker) -> None:
-        if c.ctx:  # (a context closed by its own finalizer is not reused)
+    def _give_chunker(self, c) -> None:
+        if getattr(c, "ctx", None) or getattr(c, "g", None):  # (not closed by a finalizer)
             self._idle.append(c)
 
     def trim(self) -> dict:
@@ -93,7 +102,8 @@ class UnorderedWriter:
         self.lib = _lib.load()
         self._storage = storage
         self._chunker = storage._take_chunker()
-        self.events: list = []
+        self.events: list = []  # per serialized fileset, its events in arrival order
+        self.log: list = []  # every event as (fileset, ...) in arrival order
         self._exc: Optional[BaseException] = None
         # the callback reaches the writer through a weak reference: a bound method here would
         # make a reference cycle, which the cyclic GC frees in arbitrary order, closing the
@@ -107,9 +117,14 @@ class UnorderedWriter:
         self._cfun = _lib.UW_CB(on_event)
         ip = storage.index_params.to_c() if storage.index_params else None
         w = C.c_void_p()
-        rc = self.lib.pfscdc_uw_create(self._chunker.ctx, storage.mem_threshold,
-                                       C.byref(ip) if ip is not None else None, self._cfun, None,
-                                       C.byref(w))
+        if storage.devices is not None:
+            rc = self.lib.pfscdc_uw_create_group(self._chunker.g, storage.mem_threshold,
+                                                 C.byref(ip) if ip is not None else None,
+                                                 self._cfun, None, C.byref(w))
+        else:
+            rc = self.lib.pfscdc_uw_create(self._chunker.ctx, storage.mem_threshold,
+                                           C.byref(ip) if ip is not None else None, self._cfun,
+                                           None, C.byref(w))
         if rc:
             raise _lib.PfsCdcError(rc, "pfscdc_uw_create")
         self._w = w
@@ -121,11 +136,12 @@ class UnorderedWriter:
                 self.events.append([])
             if ev.kind == _lib.EV_CHUNK:
                 ch = ev.chunk
-                self.events[ev.fileset].append(
-                    ("chunk", ev.index, ev.level if ev.index >= 0 else 0, ch.size_bytes,
-                     bool(ch.edge), bytes(ch.ref.id)))
+                e = ("chunk", ev.index, ev.level if ev.index >= 0 else 0, ch.size_bytes,
+                     bool(ch.edge), bytes(ch.ref.id))
             else:
-                self.events[ev.fileset].append(("index", ev.index, C.string_at(ev.bytes, ev.len)))
+                e = ("index", ev.index, C.string_at(ev.bytes, ev.len))
+            self.events[ev.fileset].append(e)
+            self.log.append((ev.fileset,) + e)
             return 0
         except BaseException as e:
             self._exc = e

@@ -1,5 +1,5 @@
 /* A plain C99 driver of the host-heavy entry points, for the host-sanitizer run
- * (tools/r5_host_sanitize.sh): the UnorderedWriter (Put, append, Delete, directory deletes,
+ * (tools/host_sanitize.sh): the UnorderedWriter (Put, append, Delete, directory deletes,
  * grouped background fileset writes), the chunk store, Writer.Copy of another writer's
  * DataRefs, MergeFileReader.Hash, and four threads scanning at once, each on its own ctx.  Parity of these paths is tested from Python against the
  * oracle; this program only has to drive them through a sanitized library and print a
@@ -13,7 +13,7 @@
 
 #include "pfscdc.h"
 
-/* Under LeakSanitizer (tools/r5_host_sanitize.sh) the leak check runs here, before the HIP
+/* Under LeakSanitizer (tools/host_sanitize.sh) the leak check runs here, before the HIP
  * runtime's own teardown, and the process then leaves with _exit: at exit, ROCm's ASan device
  * allocator CHECK-fails freeing HSA runtime objects after that runtime has unloaded
  * (profiles/r5/sanitize/).  Weak: a build without the sanitizers links without it. */
