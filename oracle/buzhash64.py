@@ -21,14 +21,20 @@ from . import gorand
 _M64 = (1 << 64) - 1
 
 
-def generate_hashes(seed: int) -> list[int]:
+def generate_hashes(seed: int, draw: str = "int63") -> list[int]:
+    """A1: ``draw="int63"`` (T[i] = uint64(rand.Int63()), what the product implements).
+    ``draw="uint64"`` is the one plausible alternative (T[i] = rand.Uint64(), the full 64-bit
+    ALFG value); oracle/go_probe prints the real GenerateHashes so a Go run picks one."""
+    if draw not in ("int63", "uint64"):
+        raise ValueError(draw)
     r = gorand.Source(seed)
+    nxt = r.int63 if draw == "int63" else r.uint64
     used: set[int] = set()
     out = []
     for _ in range(256):
-        x = r.int63()
+        x = nxt()
         while x in used:
-            x = r.int63()
+            x = nxt()
         used.add(x)
         out.append(x)
     return out

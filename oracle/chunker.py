@@ -66,13 +66,34 @@ class Params:
         return (1 << self.average_bits) - 1
 
 
-_TABLES: dict[int, list[int]] = {}
+_TABLES: dict[tuple, list[int]] = {}
+TABLE_DRAW = "int63"  # assumption A1 (buzhash64.generate_hashes); "uint64" only for go_probe
 
 
 def table(seed: int) -> list[int]:
-    if seed not in _TABLES:
-        _TABLES[seed] = buzhash64.generate_hashes(seed)
-    return _TABLES[seed]
+    key = (TABLE_DRAW, seed)
+    if key not in _TABLES:
+        _TABLES[key] = buzhash64.generate_hashes(seed, TABLE_DRAW)
+    return _TABLES[key]
+
+
+class table_draw:
+    """``with table_draw("uint64"): ...`` runs the oracle under the other A1 variant."""
+
+    def __init__(self, draw: str):
+        if draw not in ("int63", "uint64"):
+            raise ValueError(draw)
+        self.draw = draw
+
+    def __enter__(self):
+        global TABLE_DRAW
+        self.old, TABLE_DRAW = TABLE_DRAW, self.draw
+        return self
+
+    def __exit__(self, *exc):
+        global TABLE_DRAW
+        TABLE_DRAW = self.old
+        return False
 
 
 @dataclass
