@@ -65,14 +65,19 @@ def parse():
     ap.add_argument("--ref-ids", action="store_true",
                     help="also compute every chunk's Ref (Id = BLAKE2b(ChaCha20_dek(chunk)), "
                          "§8 next row 1) inside the step")
-    ap.add_argument("--path", default="put", choices=["put", "get", "commit", "uw", "rechunk"],
+    ap.add_argument("--path", default="put",
+                    choices=["put", "get", "commit", "uw", "rechunk", "group"],
                     help="put: the ingest path (default); get: chunk.Get of the step's chunks "
                          "(verify BLAKE2b of the stored bytes against Ref.Id, ChaCha20 "
                          "decrypt), §8 next row 3, device-resident in and out; commit: the "
                          "pachd data plane, §8 next rows 1-3: files cut into filesets at "
                          "--mem-threshold bytes, one chunk.Writer stream per fileset (Annotate "
                          "cut, CDC cuts, Close), chunk.Create (Ref.Id/Dek) per formed chunk; "
-                         "uw: host-fed UnorderedWriter with indexes; rechunk: Writer.Copy")
+                         "uw: host-fed UnorderedWriter with indexes; rechunk: Writer.Copy; "
+                         "group: one process driving a device group (pfscdc_group_*)")
+    ap.add_argument("--members", default="",
+                    help="--path group: member devices, e.g. 0,1,2,3 or 0,0,0,0 (default: every "
+                         "visible device once)")
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
     ap.add_argument("--uw-workers", type=int, default=0,
@@ -234,6 +239,9 @@ def main():
     if args.path == "uw":
         from benchkit.uw import bench_uw
         return bench_uw(args, ctx)
+    if args.path == "group":
+        from benchkit.group import bench_group
+        return bench_group(args, ctx)
     if args.path == "rechunk":
         from benchkit.rechunk import bench_rechunk
         return bench_rechunk(args, ctx)
