@@ -186,7 +186,7 @@ def load_traffic(args, work):
     path = args.traffic_json
     if not path and args.config == "c2" and work.group == 32 and args.files == 1024 \
             and args.file_bytes == 4 << 20 and args.path == "put" and not args.ref_ids:
-        path = os.path.join(ROOT, "profiles", "r5", "final", "traffic_c2.json")
+        path = os.path.join(ROOT, "profiles", "r6", "final", "traffic_c2.json")
     if path and os.path.exists(path):
         tj = json.load(open(path))
         tj["_source"] = os.path.relpath(path, ROOT)
