@@ -1,7 +1,8 @@
 /* A plain C99 driver of the host-heavy entry points, for the host-sanitizer run
  * (tools/host_sanitize.sh): the UnorderedWriter (Put, append, Delete, directory deletes,
  * grouped background fileset writes), the chunk store, Writer.Copy of another writer's
- * DataRefs, MergeFileReader.Hash, and four threads scanning at once, each on its own ctx.  Parity of these paths is tested from Python against the
+ * DataRefs, MergeFileReader.Hash, four threads scanning at once, each on its own ctx, and a
+ * device group (its member threads and its unordered writer).  Parity of these paths is tested from Python against the
  * oracle; this program only has to drive them through a sanitized library and print a
  * summary.  usage: uw_consumer NFILES SEED */
 #include <inttypes.h>
@@ -222,6 +223,30 @@ int main(int argc, char** argv) {
       }
     }
     printf("threads 4 segments %" PRIu64 "\n", jobs[0].nsegs);
+    free(offs);
+  }
+  /* 5. a device group of four ctxs on device 0: the batch dealt over them and gathered, then
+   * an unordered writer over the group (four group writers, events released in group order) */
+  {
+    int devs[4] = {0, 0, 0, 0};
+    pfscdc_group* g = NULL;
+    pfscdc_uwriter* gw = NULL;
+    uint64_t* offs = (uint64_t*)calloc(nfiles + 1, sizeof *offs);
+    if (!offs) return 1;
+    for (f = 0; f < nfiles; f++) offs[f + 1] = offs[f] + lens[f];
+    OK(pfscdc_group_create(&p, devs, 4, PFSCDC_OPT_REF_IDS, &g), NULL);
+    OK(pfscdc_group_scan(g, data, total, offs, nfiles), NULL);
+    printf("group segments %" PRIu64 "\n", pfscdc_group_num_segments(g));
+    uw_events = uw_index_events = 0;
+    OK(pfscdc_uw_create_group(g, 300000, &ip, on_uw, NULL, &gw), NULL);
+    for (f = 0, k = 0; f < nfiles; k += lens[f], f++) {
+      snprintf(path, sizeof path, "/g/f%05u", f);
+      OK(pfscdc_uw_put(gw, path, "", 0, data + k, lens[f]), NULL);
+    }
+    OK(pfscdc_uw_close(gw), NULL);
+    printf("group uw filesets %u events %" PRIu64 "\n", pfscdc_uw_num_filesets(gw), uw_events);
+    OK(pfscdc_uw_destroy(gw), NULL);
+    OK(pfscdc_group_destroy(g), NULL);
     free(offs);
   }
   {
