@@ -77,7 +77,8 @@ def parse():
                          "group: one process driving a device group (pfscdc_group_*)")
     ap.add_argument("--members", default="",
                     help="--path group: member devices, e.g. 0,1,2,3 or 0,0,0,0 (default: every "
-                         "visible device once)")
+                         "visible device once); --path uw: the writer's device group (default: "
+                         "one GPU)")
     ap.add_argument("--uw-bytes", type=int, default=8 << 30,
                     help="uw: host bytes Put through the UnorderedWriter per step")
     ap.add_argument("--uw-workers", type=int, default=0,

@@ -49,7 +49,10 @@ def bench_uw(args, ctx):
         _lib.set_knob("PFSCDC_UW_WORKERS", args.uw_workers)
     if args.uw_group > 0:
         _lib.set_knob("PFSCDC_UW_INFLIGHT", args.uw_group)
-    st = pf.Storage(ctx["local"], params, args.mem_threshold)
+    members = [int(x) for x in args.members.split(",")] if args.members else None
+    if members and world > 1:
+        raise SystemExit("--members (a device group in one process) with --gpus > 1")
+    st = pf.Storage(ctx["local"], params, args.mem_threshold, devices=members)
     last = {}
 
     def step():
@@ -87,7 +90,8 @@ def bench_uw(args, ctx):
             "filesets": lay.nfilesets, "filesets_this_rank": len(prims),
             "data_chunks_this_rank": last["nchunks"], "gpu_max_hw_queues": ctx["hwq"],
             "parallelism": "fileset-sharded x%d, gather of the fileset roots" % world
-            if world > 1 else "single GPU"}
+            if world > 1 else ("device group over %s (pfscdc_uw_create_group)" % members
+                               if members else "single GPU")}
     out = H.line("GiB/s host-fed pachd write path (Put -> filesets with chunk Refs and "
                  "multilevel indexes)", bytes_step, args.steps, args.warmup, elapsed, "strong",
                  info, data="synthetic bytes in host memory",
