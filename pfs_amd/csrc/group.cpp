@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -143,8 +144,15 @@ int group_scan(pfscdc_group* g, const uint8_t* host, const void* const* member_b
     auto job = [g, k, src, on_dev, offs, pb, &rcs] {
       rcs[k] = member_scan(g->members[k], src, on_dev, offs, pb[k], pb[k + 1], &g->member_ms[k]);
     };
-    if (k + 1 == n) job();  // the caller's thread takes the last member
-    else th.emplace_back(job);
+    if (k + 1 == n) {
+      job();  // the caller's thread takes the last member
+      continue;
+    }
+    try {
+      th.emplace_back(job);
+    } catch (const std::system_error&) {
+      job();  // no thread to be had: this member runs here, before the next one starts
+    }
   }
   for (auto& t : th) t.join();
   for (uint32_t k = 0; k < n; k++)
