@@ -16,7 +16,6 @@
 // their member-local file ids rebased there, then brought to the host in one copy.
 #include <hip/hip_runtime.h>
 
-#include <chrono>
 #include <cstring>
 #include <string>
 #include <system_error>
