@@ -202,3 +202,61 @@ def test_ordered_events_with_two_group_writers(knob):
     st2 = PF.Storage(0, cp(SMALL), 250_000, cp(SMALL_INDEX))
     got, glog = uw_run(st2, ops)
     assert got == want and glog == wlog
+
+
+@pytest.mark.parametrize("case", fuzz_cases(6))
+def test_group_unordered_writer_random_ops_equal_one_ctx(case, knob):
+    """Random Put/Delete sequences (memThreshold splits, exact fills, appends, overwrites,
+    tags, file and directory deletes) over a device group of 1-8 ctxs, with the writer's own
+    forms drawn per case: the ordered event stream equals one ctx writing the same groups,
+    and the filesets equal the restated reference."""
+    from test_gpu_fileset import RAND_INDEX, random_ops
+
+    rng = np.random.default_rng(7700 + case)
+    n = int(rng.integers(1, 9))
+    thr = int(rng.integers(60_000, 400_000))
+    group = int(rng.choice([thr, 2 * thr, 3 * thr + 1]))
+    knob("PFSCDC_UW_MIRROR", int(rng.integers(0, 2)))
+    knob("PFSCDC_UW_INDEX_GROUPED", int(rng.integers(0, 2)))
+    data = synthetic_bytes([0, 8 << 20], 170 + case).tobytes()
+    paths = [f"/d{int(rng.integers(0, 3))}/s{int(rng.integers(0, 2))}/f{j:03d}"
+             for j in range(int(rng.integers(3, 40)))]
+    ops = random_ops(rng, data, int(rng.integers(40, 200)), paths, thr)
+    knob("PFSCDC_UW_INFLIGHT", group)
+    want, wlog = uw_run(PF.Storage(0, cp(SMALL), thr, cp(RAND_INDEX)), ops)
+    knob("PFSCDC_UW_INFLIGHT", group * n)
+    got, glog = uw_run(PF.Storage(0, cp(SMALL), thr, cp(RAND_INDEX), devices=[0] * n), ops)
+    assert glog == wlog
+    assert got == want
+    ow = OF.UnorderedWriter(SMALL, thr, RAND_INDEX)
+    for op in ops:
+        (ow.put if op[0] == "put" else ow.delete)(*op[1:])
+    ref = ow.close()
+    assert [(p.additive, p.deletive, p.size_bytes) for p in got] == \
+        [(r.additive, r.deletive, r.size_bytes) for r in ref]
+
+
+@pytest.mark.parametrize("case", fuzz_cases(4))
+def test_group_scan_resident_random_dealing_equal_one_ctx(case):
+    """Caller-chosen dealings (empty members, one member holding everything, uneven splits)
+    over 1-8 ctxs, with Ref ids on or off, equal one ctx over the same bytes."""
+    import torch
+
+    rng = np.random.default_rng(7900 + case)
+    n = int(rng.integers(1, 9))
+    p = [SMALL, Ch.Params(average_bits=14, seed=3, min=4000, max=90000)][case % 2]
+    nf = int(rng.integers(0, 120))
+    lens = rng.integers(0, 6 * p.max, nf)
+    lens[rng.random(nf) < 0.2] = 0
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ref_ids = bool(rng.integers(0, 2))
+    one = Chunker(cp(p), 0, ref_ids=ref_ids)
+    dev = torch.empty(max(int(offs[-1]), 1), dtype=torch.uint8, device="cuda:0")
+    one.fill_synthetic(dev, offs, 300 + case)
+    want = one.scan(dev[:int(offs[-1])], offs)
+    g = DeviceGroup([0] * n, cp(p), ref_ids=ref_ids)
+    pb = np.concatenate([[0], np.sort(rng.integers(0, nf + 1, n - 1)), [nf]]).astype(np.uint32)
+    parts = [dev[int(offs[pb[k]]):int(offs[pb[k + 1]])].clone() if pb[k + 1] > pb[k] else None
+             for k in range(n)]
+    got = g.scan_resident(parts, offs, pb)
+    same_result(want, got)
