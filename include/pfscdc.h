@@ -526,6 +526,15 @@ int pfscdc_group_scan(pfscdc_group* g, const void* bytes, uint64_t nbytes,
 int pfscdc_group_scan_resident(pfscdc_group* g, const void* const* member_bytes,
                                const uint64_t* file_offsets, uint32_t nfiles,
                                const uint32_t* part_begin);
+/* One stream (a single file of nbytes in host memory, e.g. configs[2]'s 10 GiB) split across
+ * the members, block-parallel with window-overlap stitching: member k holds an equal byte range
+ * (borders on 64-byte boundaries) plus the 64 bytes in front (the window) and up to
+ * max_chunk - 1 bytes after (for the segment that straddles its end), finds its range's
+ * candidate positions (pfscdc_candidates); the serial min/max selection (writer.go:163-189)
+ * then runs once over the gathered candidates on the host, and each segment is hashed by the
+ * member holding its first byte.  Results as for one file through the accessors below (file 0;
+ * no Refs, no dealing, no device index); equal to pfscdc_scan of the stream on one ctx. */
+int pfscdc_group_scan_stream(pfscdc_group* g, const void* bytes, uint64_t nbytes);
 /* Results of the last group scan (valid until the next one): the gathered index ordered by
  * (file, offset) with global file ids, per-file ranges (nfiles + 1), Refs (NULL unless the
  * group has PFSCDC_OPT_REF_IDS), and the dealing used (n + 1). */

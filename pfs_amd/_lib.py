@@ -59,6 +59,7 @@ EXPORTED = [
     "pfscdc_group_scan_resident", "pfscdc_group_num_segments", "pfscdc_group_segments",
     "pfscdc_group_file_segment_begin", "pfscdc_group_refs", "pfscdc_group_part_begin",
     "pfscdc_group_index_device", "pfscdc_group_last_timings", "pfscdc_uw_create_group",
+    "pfscdc_group_scan_stream",
 ]
 
 
@@ -260,6 +261,7 @@ def load() -> C.CDLL:
             "pfscdc_group_index_device": (i32, [vp, P(vp), P(vp), P(C.c_int)]),
             "pfscdc_group_last_timings": (i32, [vp, P(C.c_float), P(C.c_float), P(u64)]),
             "pfscdc_uw_create_group": (i32, [vp, i64, P(Params), UW_CB, vp, P(vp)]),
+            "pfscdc_group_scan_stream": (i32, [vp, vp, u64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -16,6 +16,8 @@
 // their member-local file ids rebased there, then brought to the host in one copy.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <system_error>
@@ -47,12 +49,24 @@ struct pfscdc_group {
   pfscdc_ref* h_refs = nullptr;
   uint64_t h_cap = 0;
   uint64_t bytes_copied = 0;  // bytes the gather moved (records + refs)
+  // pfscdc_group_scan_stream: each member's range of the stream (plus the 64-byte halo in
+  // front and up to max_chunk - 1 bytes after, for the segment that straddles its end)
+  std::vector<uint8_t*> d_stream;
+  std::vector<uint64_t> d_stream_cap;
+  std::vector<pfscdc_segment> h_stream_segs;  // the stream form's records (host)
+  bool stream_form = false;                    // the last scan was pfscdc_group_scan_stream
 
   int fail(int code, const std::string& msg) {
     err = msg;
     return code;
   }
   void release_buffers() {
+    for (size_t k = 0; k < d_stream.size(); k++)
+      if (d_stream[k]) {
+        (void)hipSetDevice(devices[k]);
+        (void)hipFree(d_stream[k]);
+        d_stream[k] = nullptr;
+      }
     if (d_index || d_refs) (void)hipSetDevice(index_device);
     if (d_index) (void)hipFree(d_index);
     if (d_refs) (void)hipFree(d_refs);
@@ -132,6 +146,7 @@ int ensure_index(pfscdc_group* g, uint64_t n, bool refs) {
 int group_scan(pfscdc_group* g, const uint8_t* host, const void* const* member_bytes,
                const uint64_t* offs, uint32_t nfiles) {
   const uint32_t n = (uint32_t)g->members.size();
+  g->stream_form = false;
   const uint32_t* pb = g->part_begin.data();
   g->member_ms.assign(n, 0.f);
   std::vector<int> rcs(n, PFSCDC_OK);
@@ -211,9 +226,168 @@ int group_scan(pfscdc_group* g, const uint8_t* host, const void* const* member_b
   return PFSCDC_OK;
 }
 
+// Writer.roll's serial cut rule (writer.go:163-189) for one annotation of n bytes over its
+// sorted candidate positions: a segment starting at s ends at the first candidate at or past
+// s + min - 1 unless s + max - 1 comes first (a forced cut); the rest is the open tail.
+void select_stream_cuts(const std::vector<uint64_t>& cands, uint64_t n, uint64_t mn, uint64_t mx,
+                        std::vector<pfscdc_segment>* out) {
+  uint64_t s = 0;
+  for (;;) {
+    const uint64_t lo = s + mn - 1, hi = s + mx - 1;
+    if (lo >= n) break;
+    const auto it = std::lower_bound(cands.begin(), cands.end(), lo);
+    const uint64_t cut = (it != cands.end() && *it <= hi) ? *it : hi;
+    if (cut >= n) break;
+    pfscdc_segment seg{};
+    seg.offset = s;
+    seg.size = cut + 1 - s;
+    seg.flags = PFSCDC_SEG_VALID | PFSCDC_SEG_CUT;
+    out->push_back(seg);
+    s = cut + 1;
+  }
+  if (s < n) {
+    pfscdc_segment seg{};
+    seg.offset = s;
+    seg.size = n - s;
+    seg.flags = PFSCDC_SEG_VALID;
+    out->push_back(seg);
+  }
+}
+
+// Runs job(k) for every member k with work, one host thread each (the caller's thread takes
+// the last), and returns the first member's failure.
+template <class F>
+int for_members(pfscdc_group* g, const std::vector<char>& busy, F job) {
+  const uint32_t n = (uint32_t)g->members.size();
+  std::vector<int> rcs(n, PFSCDC_OK);
+  std::vector<std::thread> th;
+  uint32_t last = n;
+  for (uint32_t k = 0; k < n; k++)
+    if (busy[k]) last = k;
+  for (uint32_t k = 0; k < n; k++) {
+    if (!busy[k]) continue;
+    auto run = [&, k] { rcs[k] = job(k); };
+    if (k == last) {
+      run();
+      continue;
+    }
+    try {
+      th.emplace_back(run);
+    } catch (const std::system_error&) {
+      run();
+    }
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t k = 0; k < n; k++)
+    if (rcs[k])
+      return g->fail(rcs[k], "member " + std::to_string(k) + " (device " +
+                                 std::to_string(g->devices[k]) + "): " +
+                                 pfscdc_last_error(g->members[k]));
+  return PFSCDC_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int pfscdc_group_scan_stream(pfscdc_group* g, const void* bytes, uint64_t nbytes) {
+  if (!g) return PFSCDC_EINVAL;
+  g->err.clear();
+  g->nsegs = 0;
+  g->have_refs = false;
+  if (nbytes && !bytes) return g->fail(PFSCDC_EINVAL, "bytes is NULL");
+  const uint32_t n = (uint32_t)g->members.size();
+  const pfscdc_params& p = pfscdc::ctx_params(g->members[0]);
+  const uint64_t mx = (uint64_t)p.max_chunk;
+  // equal byte ranges, borders on 64-byte boundaries (pfs_amd.distributed.split_stream)
+  std::vector<uint64_t> bound(n + 1, 0);
+  for (uint32_t r = 1; r < n; r++) {
+    const uint64_t b = (uint64_t)(((unsigned __int128)nbytes * r / n) / 64 * 64);
+    bound[r] = std::max(bound[r - 1], std::min(b, nbytes));
+  }
+  bound[n] = nbytes;
+  g->part_begin.clear();  // one file split by bytes: no file dealing to report
+  g->d_stream.resize(n, nullptr);
+  g->d_stream_cap.resize(n, 0);
+  std::vector<char> busy(n, 0);
+  for (uint32_t k = 0; k < n; k++) busy[k] = bound[k + 1] > bound[k];
+  const uint8_t* src = (const uint8_t*)bytes;
+  g->member_ms.assign(n, 0.f);
+  using clk = std::chrono::steady_clock;
+  // 1. every member's candidates, from its bytes plus the halo in front (the bytes after its
+  // range, up to max - 1, come along for the hash of the segment that straddles its end)
+  std::vector<std::vector<uint64_t>> cands(n);
+  std::vector<clk::time_point> t0(n);
+  int rc = for_members(g, busy, [&](uint32_t k) -> int {
+    t0[k] = clk::now();
+    const uint64_t a = bound[k], b = bound[k + 1], h = std::min<uint64_t>(64, a);
+    const uint64_t end = std::min<uint64_t>(nbytes, b + mx), len = end - (a - h);
+    if (hipSetDevice(g->devices[k]) != hipSuccess) return PFSCDC_EHIP;
+    if (len > g->d_stream_cap[k]) {
+      if (g->d_stream[k]) (void)hipFree(g->d_stream[k]);
+      g->d_stream[k] = nullptr;
+      g->d_stream_cap[k] = 0;
+      if (hipMalloc((void**)&g->d_stream[k], len) != hipSuccess) return PFSCDC_ENOMEM;
+      g->d_stream_cap[k] = len;
+    }
+    if (hipMemcpy(g->d_stream[k], src + (a - h), len, hipMemcpyHostToDevice) != hipSuccess)
+      return PFSCDC_EHIP;
+    uint64_t cap = (b - a) / 4096 + 64, got = 0;
+    for (;;) {
+      cands[k].resize(cap);
+      const int r = pfscdc_candidates(g->members[k], g->d_stream[k], (b - a) + h, 1, h,
+                                      cands[k].data(), cap, &got);
+      if (r == PFSCDC_ENOMEM && got > cap) {
+        cap = got;
+        continue;
+      }
+      if (r) return r;
+      break;
+    }
+    cands[k].resize(got);
+    for (uint64_t& c : cands[k]) c += a - h;  // stream offsets
+    return PFSCDC_OK;
+  });
+  if (rc) return rc;
+  // 2. the serial selection over the gathered, sorted candidates (ranges are in stream order)
+  std::vector<uint64_t> all;
+  for (const auto& v : cands) all.insert(all.end(), v.begin(), v.end());
+  std::vector<pfscdc_segment> segs;
+  select_stream_cuts(all, nbytes, (uint64_t)p.min_chunk, mx, &segs);
+  // 3. each segment hashed by the member holding its first byte
+  std::vector<uint64_t> first(n + 1, 0);
+  for (uint32_t k = 0, i = 0; k <= n; k++) {
+    while (k < n && i < segs.size() && segs[i].offset < bound[k]) i++;
+    first[k] = k < n ? i : segs.size();
+  }
+  rc = for_members(g, busy, [&](uint32_t k) -> int {
+    const uint64_t a = bound[k], h = std::min<uint64_t>(64, a);
+    const uint64_t i0 = first[k], i1 = first[k + 1];
+    if (i1 > i0) {
+      std::vector<uint64_t> begins(i1 - i0), sizes(i1 - i0);
+      for (uint64_t i = i0; i < i1; i++) {
+        begins[i - i0] = segs[i].offset - (a - h);
+        sizes[i - i0] = segs[i].size;
+      }
+      std::vector<uint8_t> out(32 * (i1 - i0));
+      const uint64_t len = std::min<uint64_t>(nbytes, bound[k + 1] + mx) - (a - h);
+      const int r = pfscdc_hash_ranges(g->members[k], g->d_stream[k], len, 1, begins.data(),
+                                       sizes.data(), (uint32_t)(i1 - i0), out.data());
+      if (r) return r;
+      for (uint64_t i = i0; i < i1; i++) std::memcpy(segs[i].hash, &out[32 * (i - i0)], 32);
+    }
+    g->member_ms[k] = std::chrono::duration<float, std::milli>(clk::now() - t0[k]).count();
+    return PFSCDC_OK;
+  });
+  if (rc) return rc;
+  g->h_stream_segs.swap(segs);
+  g->stream_form = true;
+  g->nsegs = g->h_stream_segs.size();
+  g->seg_begin.assign({0, g->nsegs});
+  g->gather_ms = 0.f;
+  g->bytes_copied = 0;
+  return PFSCDC_OK;
+}
 
 int pfscdc_deal(const uint64_t* offsets, uint32_t nitems, uint32_t nparts, uint32_t* part_begin) {
   if (!offsets || !part_begin || nparts == 0) return PFSCDC_EINVAL;
@@ -352,7 +526,8 @@ int pfscdc_group_scan_resident(pfscdc_group* g, const void* const* member_bytes,
 uint64_t pfscdc_group_num_segments(const pfscdc_group* g) { return g ? g->nsegs : 0; }
 
 const pfscdc_segment* pfscdc_group_segments(const pfscdc_group* g) {
-  return g && g->nsegs ? g->h_index : nullptr;
+  if (!g || !g->nsegs) return nullptr;
+  return g->stream_form ? g->h_stream_segs.data() : g->h_index;
 }
 
 const uint64_t* pfscdc_group_file_segment_begin(const pfscdc_group* g) {
@@ -370,8 +545,8 @@ const uint32_t* pfscdc_group_part_begin(const pfscdc_group* g) {
 int pfscdc_group_index_device(const pfscdc_group* g, const pfscdc_segment** segs,
                               const pfscdc_ref** refs, int* device) {
   if (!g) return PFSCDC_EINVAL;
-  if (segs) *segs = g->nsegs ? g->d_index : nullptr;
-  if (refs) *refs = g->nsegs && g->have_refs ? g->d_refs : nullptr;
+  if (segs) *segs = g->nsegs && !g->stream_form ? g->d_index : nullptr;
+  if (refs) *refs = g->nsegs && g->have_refs && !g->stream_form ? g->d_refs : nullptr;
   if (device) *device = g->index_device;
   return PFSCDC_OK;
 }

@@ -85,10 +85,10 @@ class DeviceGroup:
                 if (n and rp) else np.zeros(0, dtype=rdt)
         return ScanResult(segs, begin, refs=refs)
 
-    def part_begin(self) -> np.ndarray:
-        """The dealing of the last scan (n + 1 entries)."""
+    def part_begin(self) -> Optional[np.ndarray]:
+        """The dealing of the last scan (n + 1 entries; None after a stream scan)."""
         p = self.lib.pfscdc_group_part_begin(self.g)
-        return np.ctypeslib.as_array(p, shape=(len(self) + 1,)).copy()
+        return np.ctypeslib.as_array(p, shape=(len(self) + 1,)).copy() if p else None
 
     def scan(self, data, file_offsets: Sequence[int]) -> ScanResult:
         """pfscdc_group_scan over host bytes (bytes/bytearray/np.uint8)."""
@@ -99,6 +99,15 @@ class DeviceGroup:
                                         offs.ctypes.data_as(C.POINTER(C.c_uint64)), len(offs) - 1)
         self._check(rc, "group_scan")
         return self._result(len(offs) - 1)
+
+    def scan_stream(self, data) -> ScanResult:
+        """pfscdc_group_scan_stream: one stream (host bytes) split across the members."""
+        arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+            else np.ascontiguousarray(data, dtype=np.uint8)
+        rc = self.lib.pfscdc_group_scan_stream(self.g, arr.ctypes.data if arr.size else None,
+                                               arr.size)
+        self._check(rc, "group_scan_stream")
+        return self._result(1)
 
     def scan_resident(self, member_bytes: Sequence, file_offsets: Sequence[int],
                       part_begin: Optional[Sequence[int]] = None) -> ScanResult:

@@ -9,6 +9,9 @@
  *      field by field with pfscdc_scan on one ctx; prints the group's dealing and records:
  *        part K BEGIN END
  *        seg FILE OFFSET SIZE FLAGS HASH ID DEK
+ *   1b. the whole batch as one stream, pfscdc_group_scan_stream against pfscdc_scan of one
+ *      file:
+ *        stream SEGMENTS
  *   2. pfscdc_uw_create_group (Puts of every file as /f%05u) against pfscdc_uw_create on one
  *      ctx: the one ctx writes groups of INFLIGHT bytes, the group INFLIGHT * NDEV split over
  *      NDEV members, so both form the same groups; the ordered event streams and every
@@ -177,6 +180,21 @@ int main(int argc, char** argv) {
       hex(ref[i].dek, 32);
       printf("\n");
     }
+  }
+
+  /* 1b. the whole batch as one stream split across the group, against one ctx */
+  {
+    uint64_t one_offs[2] = {0, total};
+    if (pfscdc_scan(one, data, total, 0, one_offs, 1) != PFSCDC_OK)
+      DIE("scan stream", pfscdc_last_error(one));
+    if (pfscdc_group_scan_stream(g, data, total) != PFSCDC_OK)
+      DIE("group_scan_stream", pfscdc_group_last_error(g));
+    if (pfscdc_group_num_segments(g) != pfscdc_num_segments(one) ||
+        (pfscdc_num_segments(one) &&
+         memcmp(pfscdc_group_segments(g), pfscdc_segments(one),
+                pfscdc_num_segments(one) * sizeof(pfscdc_segment)) != 0))
+      DIE("stream records differ", "");
+    printf("stream %" PRIu64 "\n", pfscdc_group_num_segments(g));
   }
 
   /* 2. the unordered writer: one ctx against the group */

@@ -127,5 +127,6 @@ def test_c_process_drives_a_device_group(group_consumer, tmp_path, ndev):
         assert [int(x) for x in g[:4]] == [int(s["file"]), int(s["offset"]), int(s["size"]),
                                           int(s["flags"])]
         assert g[4] == bytes(s["hash"]).hex()
+    assert len([ln for ln in lines if ln.startswith("stream ")]) == 1
     uw = [ln.split() for ln in lines if ln.startswith("uw ")]
     assert len(uw) == 1 and int(uw[0][1]) > 0 and int(uw[0][2]) >= 2 * ndev

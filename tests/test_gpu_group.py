@@ -260,3 +260,37 @@ def test_group_scan_resident_random_dealing_equal_one_ctx(case):
              for k in range(n)]
     got = g.scan_resident(parts, offs, pb)
     same_result(want, got)
+
+
+@pytest.mark.parametrize("case", fuzz_cases(6))
+def test_group_scan_stream_equals_one_ctx(case):
+    """One stream split across 1-8 ctxs (equal byte ranges, the 64-byte window in front, the
+    serial selection over the gathered candidates, each segment hashed by the member holding
+    its first byte) equals one ctx's scan of the stream: random bytes, dense candidates, and a
+    run of zeros whose forced max-size cuts straddle the members' borders."""
+    rng = np.random.default_rng(8100 + case)
+    n = int(rng.integers(1, 9))
+    p = [SMALL, Ch.Params(average_bits=8, seed=2, min=64, max=3000),
+         Ch.Params(average_bits=14, seed=1, min=5000, max=40000)][case % 3]
+    nb = int(rng.integers(0, 3 << 20)) if case % 4 else int(rng.integers(0, 200))
+    data = synthetic_bytes([0, nb], 500 + case)
+    if case % 2 and nb > 1000:
+        a = int(rng.integers(0, nb // 2))
+        data[a:a + int(rng.integers(1, nb - a))] = 0  # forced cuts at max inside the zero run
+    one = Chunker(cp(p), 0)
+    want = one.scan(data, [0, nb])
+    g = DeviceGroup([0] * n, cp(p))
+    got = g.scan_stream(data)
+    same_result(want, got)
+    assert g.part_begin() is None
+
+
+def test_group_scan_stream_reference_params():
+    """configs[2]'s shape at 64 MiB: the reference chunking, four ctxs, forced 20 MB cuts."""
+    data = synthetic_bytes([0, 64 << 20], 0xC3)
+    data[20 << 20:50 << 20] = 7  # a constant run: forced cuts at 20 MB
+    one = Chunker(ChunkParams(), 0)
+    want = one.scan(data, [0, len(data)])
+    got = DeviceGroup([0, 0, 0, 0], ChunkParams()).scan_stream(data)
+    same_result(want, got)
+    assert any(int(s) == 20_000_000 for s in got.segments["size"])
